@@ -1,0 +1,625 @@
+// surfhip_api.hip -- the C-ABI of libsurfhip.so (declared in include/surfhip.h).
+//
+// Host orchestration of the detect+describe path.  The reference does this
+// per frame in Surfor::detectAndCompute (surf.cpp:205-355) with 22 symbol
+// uploads, 4 blocking syncs, a cudaMalloc and two scratch memsets per frame;
+// here a detector derives every parameter once at creation, owns HBM scratch
+// for a whole batch of frames, and enqueues ~14 launches per batch on its own
+// stream with no host synchronisation.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "surfhip.h"
+#include "surfhip_internal.h"
+
+using namespace surfhip;
+
+static_assert(sizeof(surfhip_point) == 48, "SurfPoint layout (surf_structures.h:10-30)");
+static_assert(sizeof(surfhip_param) == 48, "SurfParam layout (surf_structures.h:45-72)");
+static_assert(offsetof(surfhip_param, doubled) == 8 && offsetof(surfhip_param, upright) == 28 &&
+              offsetof(surfhip_param, extend) == 29 && offsetof(surfhip_param, nfeatures) == 44,
+              "SurfParam field offsets");
+static_assert(offsetof(surfhip_point, o) == 12 && offsetof(surfhip_point, laplace) == 20 &&
+              offsetof(surfhip_point, ori) == 24 && offsetof(surfhip_point, ambiguity) == 44,
+              "SurfPoint field offsets");
+
+static thread_local hipError_t g_last_hip = hipSuccess;
+
+#define HIPCHK(x)                                    \
+    do {                                             \
+        hipError_t e_ = (x);                         \
+        if (e_ != hipSuccess) {                      \
+            g_last_hip = e_;                         \
+            return SURFHIP_ERR_HIP;                  \
+        }                                            \
+    } while (0)
+
+static inline int align_up(int a, int b) { return (a % b != 0) ? (a - a % b + b) : a; }  // cuda_utils.h:160-163
+
+struct surfhip_detector {
+    int dev = 0;
+    hipStream_t stream = nullptr;
+    surfhip_param param{};
+    FrameParams P{};
+    OctaveParams oct[kMaxOct]{};
+    int W = 0, H = 0, max_batch = 0, max_pts = 0, cap = 0;
+    int nbands = 0, CW = 0;
+    size_t tot_osize = 0;
+    int32_t* ii = nullptr;
+    float* resp = nullptr;
+    uint32_t* colsum = nullptr;
+    surfhip_point* cand = nullptr;
+    uint32_t* keys = nullptr;
+    uint64_t* gscratch = nullptr;
+    int* cand_count = nullptr;
+    int* offsets = nullptr;
+    int* status = nullptr;
+    // single-frame API slots
+    surfhip_point* pts1 = nullptr;
+    float* desc1 = nullptr;
+    int* count1 = nullptr;
+    bool profiling = false;
+    hipEvent_t ev[SURFHIP_NSTAGE]{};
+    float stage_ms[SURFHIP_NSTAGE]{};
+    int last_nframes = 0;
+    long long hess_bytes = 0;
+};
+
+extern "C" {
+
+// ---------------------------------------------------------------- runtime
+
+const char* surfhip_error_string(int status)
+{
+    switch (status) {
+        case SURFHIP_OK: return "no error";
+        case SURFHIP_ERR_INVALID: return "invalid argument";
+        case SURFHIP_ERR_HIP: return hipGetErrorString(g_last_hip);
+        case SURFHIP_ERR_CAPACITY: return "candidate capacity exceeded";
+        case SURFHIP_ERR_UNSUPPORTED: return "unsupported option";
+        case SURFHIP_ERR_NOMEM: return "out of memory";
+        default: return "unknown error";
+    }
+}
+
+int surfhip_last_hip_error(void) { return (int)g_last_hip; }
+
+int surfhip_get_device_count(int* count)
+{
+    HIPCHK(hipGetDeviceCount(count));
+    return SURFHIP_OK;
+}
+int surfhip_set_device(int dev)
+{
+    HIPCHK(hipSetDevice(dev));
+    return SURFHIP_OK;
+}
+int surfhip_get_device(int* dev)
+{
+    HIPCHK(hipGetDevice(dev));
+    return SURFHIP_OK;
+}
+int surfhip_device_name(int dev, char* buf, int len, int* cu_count)
+{
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, dev));
+    if (buf && len > 0) {
+        snprintf(buf, (size_t)len, "%s (%s)", prop.name, prop.gcnArchName);
+    }
+    if (cu_count) *cu_count = prop.multiProcessorCount;
+    return SURFHIP_OK;
+}
+int surfhip_versions(int* driver, int* runtime)
+{
+    HIPCHK(hipDriverGetVersion(driver));
+    HIPCHK(hipRuntimeGetVersion(runtime));
+    return SURFHIP_OK;
+}
+int surfhip_malloc(void** ptr, size_t bytes)
+{
+    HIPCHK(hipMalloc(ptr, bytes));
+    return SURFHIP_OK;
+}
+int surfhip_malloc_pitch(void** ptr, size_t* pitch, size_t width_bytes, size_t height)
+{
+    HIPCHK(hipMallocPitch(ptr, pitch, width_bytes, height));
+    return SURFHIP_OK;
+}
+int surfhip_free(void* ptr)
+{
+    HIPCHK(hipFree(ptr));
+    return SURFHIP_OK;
+}
+int surfhip_memset(void* ptr, int value, size_t bytes)
+{
+    HIPCHK(hipMemset(ptr, value, bytes));
+    return SURFHIP_OK;
+}
+int surfhip_memset_async(void* ptr, int value, size_t bytes, void* stream)
+{
+    HIPCHK(hipMemsetAsync(ptr, value, bytes, (hipStream_t)stream));
+    return SURFHIP_OK;
+}
+static hipMemcpyKind kind_of(int k)
+{
+    switch (k) {
+        case SURFHIP_H2H: return hipMemcpyHostToHost;
+        case SURFHIP_H2D: return hipMemcpyHostToDevice;
+        case SURFHIP_D2H: return hipMemcpyDeviceToHost;
+        case SURFHIP_D2D: return hipMemcpyDeviceToDevice;
+        default: return hipMemcpyDefault;
+    }
+}
+int surfhip_memcpy(void* dst, const void* src, size_t bytes, int kind)
+{
+    HIPCHK(hipMemcpy(dst, src, bytes, kind_of(kind)));
+    return SURFHIP_OK;
+}
+int surfhip_memcpy_async(void* dst, const void* src, size_t bytes, int kind, void* stream)
+{
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, kind_of(kind), (hipStream_t)stream));
+    return SURFHIP_OK;
+}
+int surfhip_memcpy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width_bytes,
+                     size_t height, int kind)
+{
+    HIPCHK(hipMemcpy2D(dst, dpitch, src, spitch, width_bytes, height, kind_of(kind)));
+    return SURFHIP_OK;
+}
+int surfhip_device_synchronize(void)
+{
+    HIPCHK(hipDeviceSynchronize());
+    return SURFHIP_OK;
+}
+int surfhip_device_reset(void)
+{
+    HIPCHK(hipDeviceReset());
+    return SURFHIP_OK;
+}
+int surfhip_stream_create(void** stream)
+{
+    hipStream_t s;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = (void*)s;
+    return SURFHIP_OK;
+}
+int surfhip_stream_destroy(void* stream)
+{
+    HIPCHK(hipStreamDestroy((hipStream_t)stream));
+    return SURFHIP_OK;
+}
+int surfhip_stream_synchronize(void* stream)
+{
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    return SURFHIP_OK;
+}
+int surfhip_event_create(void** ev)
+{
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    *ev = (void*)e;
+    return SURFHIP_OK;
+}
+int surfhip_event_destroy(void* ev)
+{
+    HIPCHK(hipEventDestroy((hipEvent_t)ev));
+    return SURFHIP_OK;
+}
+int surfhip_event_record(void* ev, void* stream)
+{
+    HIPCHK(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream));
+    return SURFHIP_OK;
+}
+int surfhip_event_synchronize(void* ev)
+{
+    HIPCHK(hipEventSynchronize((hipEvent_t)ev));
+    return SURFHIP_OK;
+}
+int surfhip_event_elapsed(float* ms, void* start, void* stop)
+{
+    HIPCHK(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+    return SURFHIP_OK;
+}
+
+// --------------------------------------------------------------- detector
+
+// Surfor::init (surf.cpp:63-79).
+int surfhip_make_param(surfhip_param* out, int noctaves, float thresh, int doubled, int init_mask_size,
+                       int sampling_step, int upright, int extend, int desc_wsz)
+{
+    if (!out) return SURFHIP_ERR_INVALID;
+    memset(out, 0, sizeof(*out));
+    if (doubled) return SURFHIP_ERR_UNSUPPORTED;   // doubled-image integral: SURVEY.md 8f rank 2
+    if (noctaves < 1 || noctaves > kMaxOct || desc_wsz < 1 || 12 % desc_wsz != 0 || sampling_step < 1)
+        return SURFHIP_ERR_INVALID;
+    out->doubled = false;
+    out->noctaves = noctaves;
+    out->divisor = 1.f;
+    out->init_lobe = init_mask_size / 3;
+    out->max_scale = out->init_lobe + 2;
+    out->sampling = sampling_step;
+    out->thresh = thresh;
+    out->upright = upright != 0;
+    out->extend = extend != 0;
+    out->desc_wsz = desc_wsz;
+    out->mag_factor = 12 / desc_wsz;
+    out->orient_size = 4 + (extend ? 4 : 0);
+    out->nfeatures = desc_wsz * desc_wsz * out->orient_size;
+    // the NMS kernel's two 2x2x2 levels (k = 1, 3) assume 5 scales per octave
+    if (out->max_scale != 5) return SURFHIP_ERR_UNSUPPORTED;
+    if (out->nfeatures > 128) return SURFHIP_ERR_UNSUPPORTED;
+    return SURFHIP_OK;
+}
+
+// Geometry (surf.cpp:374-392) and the host parameter recurrences
+// (surf.cpp:240-292, surfd.cu:2844-2865, 3062-3076).
+static int derive(surfhip_detector* d)
+{
+    const surfhip_param& p = d->param;
+    FrameParams& P = d->P;
+    P.W = d->W;
+    P.H = d->H;
+    const int iw = d->W + 1, ih = d->H + 1;
+    P.ip = align_up(iw, 128);
+    P.iH = ih;
+    P.ii_stride = (long long)ih * P.ip;
+    P.max_scale = p.max_scale;
+    P.init_lobe = p.init_lobe;
+    P.sampling = p.sampling;
+    P.noct = p.noctaves;
+    P.thresh = p.thresh;
+    P.divisor = p.divisor;
+    P.upright = p.upright;
+    P.extend = p.extend;
+    P.wsz = p.desc_wsz;
+    P.mag = p.mag_factor;
+    P.osz = p.orient_size;
+    P.nfeat = p.nfeatures;
+
+    int sw[kMaxOct], sh[kMaxOct], sp[kMaxOct];
+    long long off = 0;
+    for (int o = 0; o < p.noctaves; o++) {
+        sw[o] = o == 0 ? (iw - 1) / p.sampling : sw[o - 1] >> 1;
+        sh[o] = o == 0 ? (ih - 1) / p.sampling : sh[o - 1] >> 1;
+        sp[o] = align_up(std::max(sw[o], 1), 128);
+        OctaveParams& q = d->oct[o];
+        q.sw = sw[o];
+        q.sh = sh[o];
+        q.sp = sp[o];
+        q.osize = sh[o] * sp[o];
+        q.ooff = off;
+        off += (long long)q.osize * p.max_scale;
+    }
+    P.resp_stride = off;
+    d->tot_osize = (size_t)off;
+
+    int mask_size = p.init_lobe - 2;
+    int octave = 1;
+    int borders[kMaxScale] = {0};
+    long long hbytes = 0;
+    for (int o = 0; o < p.noctaves; o++) {
+        OctaveParams& q = d->oct[o];
+        int s, border1;
+        if (o > 0) {
+            border1 = ((3 * (mask_size + 4 * octave)) / 2) / (p.sampling * octave) + 1;
+            borders[0] = border1;
+            borders[1] = border1;
+            s = 2;
+            q.psp = d->oct[o - 1].sp;
+            q.posize = d->oct[o - 1].osize;
+            q.pooff = d->oct[o - 1].ooff;
+        } else {
+            border1 = ((3 * (mask_size + 6 * octave)) / 2) / (p.sampling * octave) + 1;
+            s = 0;
+        }
+        q.octave = octave;
+        q.init_scale = s;
+        q.nscale = p.max_scale - s;
+        q.delta = p.sampling * octave;
+        for (int i = 0, ss = s; ss < p.max_scale; i++, ss++) {
+            borders[ss] = border1;
+            const int m = mask_size + 2 * octave * (i + 1);
+            if (ss > 2) border1 = 3 * m / 2 / q.delta + 1;
+            q.mask[i] = m;
+            q.b1[i] = border1;
+            float nrm = 9.f / (float)(m * m);
+            nrm *= nrm;
+            q.norm[i] = nrm;
+            q.x2[i] = m / 2;
+            q.x3[i] = q.x2[i] + q.x2[i];
+            q.x4[i] = q.x2[i] + q.x3[i];
+            // every box corner inside the integral image (the reference never checks)
+            const int reach = std::max(m + q.x2[i], q.x4[i]);
+            const int vx = q.sw - 2 * border1, vy = q.sh - 2 * border1;
+            if (vx > 0 && vy > 0) {
+                if (q.delta * border1 - reach < 0 || q.delta * (q.sw - border1 - 1) + reach + 1 >= iw ||
+                    q.delta * (q.sh - border1 - 1) + reach + 1 >= ih)
+                    return SURFHIP_ERR_INVALID;
+                hbytes += (long long)vx * vy * 4;
+            }
+        }
+        mask_size = q.mask[q.nscale - 1];
+        for (int k = 0; k < kMaxScale; k++) q.borders[k] = borders[k];
+        int n = 0, maxw = 0, maxh = 0;
+        for (int k = 1; k < p.max_scale - 1; k += 2) {
+            q.mb[n] = borders[k + 1] + 1;
+            const int b = q.mb[n] + q.mb[n];
+            maxw = std::max(maxw, q.sw - b);
+            maxh = std::max(maxh, q.sh - b);
+            n++;
+        }
+        q.nms_gx = ((maxw / 2 + 16 - 1) / 16) * 16;   // DX = 16, surfd.cu:3060, 3076
+        q.nms_gy = ((maxh / 2 + 16 - 1) / 16) * 16;
+        octave += octave;
+    }
+    // compulsory Hessian bytes: the integral image read once + valid responses
+    d->hess_bytes = (long long)iw * ih * 4 + hbytes;
+    return SURFHIP_OK;
+}
+
+static void free_all(surfhip_detector* d)
+{
+    void* ptrs[] = {d->ii, d->resp, d->colsum, d->cand, d->keys, d->gscratch, d->cand_count,
+                    d->offsets, d->status, d->pts1, d->desc1, d->count1};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    for (int i = 0; i < SURFHIP_NSTAGE; i++)
+        if (d->ev[i]) (void)hipEventDestroy(d->ev[i]);
+}
+
+int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, int width, int height,
+                            int max_batch, int max_pts, int cand_cap, void* stream)
+{
+    if (!out || !param || width < 16 || height < 16 || max_batch < 1 || max_pts < 1) return SURFHIP_ERR_INVALID;
+    if (width + 1 > 4096) return SURFHIP_ERR_UNSUPPORTED;     // integral kernel: <= 16 columns per thread
+    surfhip_param chk;
+    int rc = surfhip_make_param(&chk, param->noctaves, param->thresh, param->doubled, param->init_lobe * 3,
+                                param->sampling, param->upright, param->extend, param->desc_wsz);
+    if (rc != SURFHIP_OK) return rc;
+    surfhip_detector* d = new surfhip_detector();
+    d->param = chk;
+    d->W = width;
+    d->H = height;
+    d->max_batch = max_batch;
+    d->max_pts = max_pts;
+    int cap = cand_cap > 0 ? cand_cap : std::max(max_pts, kSortCap);
+    int c2 = 1;
+    while (c2 < cap) c2 <<= 1;
+    d->cap = c2;
+    d->stream = (hipStream_t)stream;
+    hipError_t e = hipGetDevice(&d->dev);
+    rc = (e == hipSuccess) ? derive(d) : SURFHIP_ERR_HIP;
+    if (rc != SURFHIP_OK) {
+        if (e != hipSuccess) g_last_hip = e;
+        delete d;
+        return rc;
+    }
+    d->nbands = (height + kBandRows - 1) / kBandRows;
+    d->CW = (width + 1 <= 2048) ? 2048 : 4096;
+    const size_t B = (size_t)max_batch;
+#define ALLOC(ptr, bytes)                                    \
+    do {                                                     \
+        e = hipMalloc((void**)&(ptr), (bytes));              \
+        if (e != hipSuccess) goto fail;                      \
+    } while (0)
+    ALLOC(d->ii, B * d->P.ii_stride * sizeof(int32_t));
+    ALLOC(d->resp, B * d->tot_osize * sizeof(float));
+    ALLOC(d->colsum, B * d->nbands * d->CW * sizeof(uint32_t));
+    ALLOC(d->cand, B * d->cap * sizeof(surfhip_point));
+    ALLOC(d->keys, B * d->cap * sizeof(uint32_t));
+    ALLOC(d->cand_count, B * sizeof(int));
+    ALLOC(d->offsets, (B + 1) * sizeof(int));
+    ALLOC(d->status, 16);
+    ALLOC(d->pts1, (size_t)max_pts * sizeof(surfhip_point));
+    ALLOC(d->desc1, (size_t)max_pts * d->param.nfeatures * sizeof(float));
+    ALLOC(d->count1, 16);
+    if (d->cap > kSortCap) ALLOC(d->gscratch, B * d->cap * sizeof(uint64_t));
+#undef ALLOC
+    // zero once: integral pad columns and response pad columns are never
+    // written by the kernels and never read by them either
+    e = hipMemset(d->ii, 0, B * d->P.ii_stride * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemset(d->resp, 0, B * d->tot_osize * sizeof(float));
+    if (e == hipSuccess) e = hipMemset(d->status, 0, 16);
+    if (e != hipSuccess) goto fail;
+    {
+        // LUTs (surf.cpp:358-371) and orientation bins (surf.cpp:83-89); the
+        // values are geometry-independent, so one constant table serves all
+        Tables t;
+        for (int n = 0; n < 83; n++) t.lut1[n] = expf(-(n + 0.5f) / 12.5f);
+        for (int n = 0; n < 40; n++) t.lut2[n] = expf(-(n + 0.5f) / 8.f);
+        t.bins[0] = (float)(-3.14159265358979323846);
+        for (int i = 1; i < 72; i++) t.bins[i] = t.bins[i - 1] + 0.08726646259971647f;
+        e = set_tables(t);
+        if (e != hipSuccess) goto fail;
+    }
+    for (int i = 0; i < SURFHIP_NSTAGE; i++) {
+        e = hipEventCreate(&d->ev[i]);
+        if (e != hipSuccess) goto fail;
+    }
+    *out = d;
+    return SURFHIP_OK;
+fail:
+    g_last_hip = e;
+    free_all(d);
+    delete d;
+    return e == hipErrorOutOfMemory ? SURFHIP_ERR_NOMEM : SURFHIP_ERR_HIP;
+}
+
+int surfhip_detector_destroy(surfhip_detector* d)
+{
+    if (!d) return SURFHIP_ERR_INVALID;
+    (void)hipStreamSynchronize(d->stream);
+    free_all(d);
+    delete d;
+    return SURFHIP_OK;
+}
+
+int surfhip_detector_set_stream(surfhip_detector* d, void* stream)
+{
+    if (!d) return SURFHIP_ERR_INVALID;
+    d->stream = (hipStream_t)stream;
+    return SURFHIP_OK;
+}
+
+static int check_frames(surfhip_detector* d, const uint8_t* frames, int nframes, int pitch, size_t stride)
+{
+    if (!d || !frames || nframes < 1 || nframes > d->max_batch) return SURFHIP_ERR_INVALID;
+    if (pitch < d->W || (pitch & 15) != 0) return SURFHIP_ERR_INVALID;
+    if (((uintptr_t)frames & 15) != 0) return SURFHIP_ERR_INVALID;
+    if (nframes > 1 && (stride < (size_t)pitch * d->H || (stride & 15) != 0)) return SURFHIP_ERR_INVALID;
+    return SURFHIP_OK;
+}
+
+int surfhip_run_integral(surfhip_detector* d, const uint8_t* frames, int nframes, int pitch, size_t stride)
+{
+    int rc = check_frames(d, frames, nframes, pitch, stride);
+    if (rc) return rc;
+    HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, d->stream));
+    return SURFHIP_OK;
+}
+
+int surfhip_run_hessian(surfhip_detector* d, int nframes)
+{
+    if (!d || nframes < 1 || nframes > d->max_batch) return SURFHIP_ERR_INVALID;
+    for (int o = 0; o < d->param.noctaves; o++)
+        HIPCHK(launch_hessian(d->ii, d->resp, nframes, d->P, d->oct[o], o, d->stream));
+    return SURFHIP_OK;
+}
+
+int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes, int pitch,
+                         size_t stride, surfhip_point* points, float* desc, int* counts)
+{
+    int rc = check_frames(d, frames, nframes, pitch, stride);
+    if (rc) return rc;
+    if (!points || !counts) return SURFHIP_ERR_INVALID;
+    hipStream_t s = d->stream;
+    const bool prof = d->profiling;
+    HIPCHK(hipMemsetAsync(d->cand_count, 0, sizeof(int) * nframes, s));
+    if (prof) HIPCHK(hipEventRecord(d->ev[0], s));
+    HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, s));
+    if (prof) HIPCHK(hipEventRecord(d->ev[1], s));
+    for (int o = 0; o < d->param.noctaves; o++)
+        HIPCHK(launch_hessian(d->ii, d->resp, nframes, d->P, d->oct[o], o, s));
+    if (prof) HIPCHK(hipEventRecord(d->ev[2], s));
+    for (int o = 0; o < d->param.noctaves; o++)
+        HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->oct[o], o, d->cand, d->keys, d->cand_count,
+                          d->cap, s));
+    if (prof) HIPCHK(hipEventRecord(d->ev[3], s));
+    HIPCHK(launch_sort(d->cand, d->keys, d->gscratch, d->cand_count, d->cap, nframes, points, d->max_pts,
+                       counts, d->offsets, d->status, s));
+    if (prof) HIPCHK(hipEventRecord(d->ev[4], s));
+    if (desc)
+        HIPCHK(launch_describe(d->ii, d->P, points, d->max_pts, counts, d->offsets, nframes, desc, s));
+    if (prof) HIPCHK(hipEventRecord(d->ev[5], s));
+    d->last_nframes = nframes;
+    return SURFHIP_OK;
+}
+
+int surfhip_detect(surfhip_detector* d, const uint8_t* image, int pitch, surfhip_point* points,
+                   int max_pts, int* num_pts, float** desc_out, int desc)
+{
+    if (!d || !points || !num_pts || max_pts < 0) return SURFHIP_ERR_INVALID;
+    int rc = surfhip_detect_batch(d, image, 1, pitch, 0, d->pts1, desc ? d->desc1 : nullptr, d->count1);
+    if (rc) return rc;
+    int cnt = 0, st = 0;
+    HIPCHK(hipMemcpyAsync(&cnt, d->count1, sizeof(int), hipMemcpyDeviceToHost, d->stream));
+    HIPCHK(hipMemcpyAsync(&st, d->status, sizeof(int), hipMemcpyDeviceToHost, d->stream));
+    HIPCHK(hipStreamSynchronize(d->stream));
+    if (st != 0) {
+        HIPCHK(hipMemsetAsync(d->status, 0, sizeof(int), d->stream));
+        return SURFHIP_ERR_CAPACITY;
+    }
+    const int n = std::min(cnt, max_pts);                  // surf.cpp:303
+    if (n > 0)
+        HIPCHK(hipMemcpyAsync(points, d->pts1, sizeof(surfhip_point) * n, hipMemcpyDeviceToDevice, d->stream));
+    if (desc && desc_out) {
+        const size_t nb = sizeof(float) * (size_t)std::max(n, 1) * d->param.nfeatures;
+        HIPCHK(hipMalloc((void**)desc_out, nb));                // cuDescribe's per-call cudaMalloc, surfd.cu:3264
+        if (n > 0)
+            HIPCHK(hipMemcpyAsync(*desc_out, d->desc1, sizeof(float) * (size_t)n * d->param.nfeatures,
+                                  hipMemcpyDeviceToDevice, d->stream));
+    }
+    HIPCHK(hipStreamSynchronize(d->stream));
+    *num_pts = n;
+    return SURFHIP_OK;
+}
+
+int surfhip_detector_candidates(surfhip_detector* d, int* h_counts, int nframes)
+{
+    if (!d || !h_counts || nframes < 1 || nframes > d->max_batch) return SURFHIP_ERR_INVALID;
+    HIPCHK(hipMemcpyAsync(h_counts, d->cand_count, sizeof(int) * nframes, hipMemcpyDeviceToHost, d->stream));
+    HIPCHK(hipStreamSynchronize(d->stream));
+    int st = 0;
+    HIPCHK(hipMemcpy(&st, d->status, sizeof(int), hipMemcpyDeviceToHost));
+    return st ? SURFHIP_ERR_CAPACITY : SURFHIP_OK;
+}
+
+int surfhip_detector_set_profiling(surfhip_detector* d, int on)
+{
+    if (!d) return SURFHIP_ERR_INVALID;
+    d->profiling = on != 0;
+    return SURFHIP_OK;
+}
+
+int surfhip_detector_stage_times(surfhip_detector* d, float* ms)
+{
+    if (!d || !ms || !d->profiling) return SURFHIP_ERR_INVALID;
+    HIPCHK(hipEventSynchronize(d->ev[SURFHIP_NSTAGE - 1]));
+    for (int i = 0; i < SURFHIP_NSTAGE - 1; i++) HIPCHK(hipEventElapsedTime(&ms[i], d->ev[i], d->ev[i + 1]));
+    HIPCHK(hipEventElapsedTime(&ms[SURFHIP_NSTAGE - 1], d->ev[0], d->ev[SURFHIP_NSTAGE - 1]));
+    return SURFHIP_OK;
+}
+
+int surfhip_detector_workspace(surfhip_detector* d, int32_t** ii, size_t* ii_stride, float** resp,
+                               size_t* resp_stride)
+{
+    if (!d) return SURFHIP_ERR_INVALID;
+    if (ii) *ii = d->ii;
+    if (ii_stride) *ii_stride = (size_t)d->P.ii_stride;
+    if (resp) *resp = d->resp;
+    if (resp_stride) *resp_stride = (size_t)d->P.resp_stride;
+    return SURFHIP_OK;
+}
+
+int surfhip_detector_geometry(surfhip_detector* d, int* iwhp, int* swhp, long long* ooff, int* osize)
+{
+    if (!d) return SURFHIP_ERR_INVALID;
+    if (iwhp) { iwhp[0] = d->W + 1; iwhp[1] = d->H + 1; iwhp[2] = d->P.ip; }
+    for (int o = 0; o < kMaxOct; o++) {
+        const bool v = o < d->param.noctaves;
+        if (swhp) { swhp[3 * o] = v ? d->oct[o].sw : 0; swhp[3 * o + 1] = v ? d->oct[o].sh : 0; swhp[3 * o + 2] = v ? d->oct[o].sp : 0; }
+        if (ooff) ooff[o] = v ? d->oct[o].ooff : 0;
+        if (osize) osize[o] = v ? d->oct[o].osize : 0;
+    }
+    return SURFHIP_OK;
+}
+
+long long surfhip_hessian_bytes_per_frame(surfhip_detector* d) { return d ? d->hess_bytes : -1; }
+
+size_t surfhip_slab_bytes(int max_pts, int nfeatures)
+{
+    const size_t b = 16 + (size_t)max_pts * sizeof(surfhip_point) + (size_t)max_pts * nfeatures * sizeof(float);
+    return (b + 255) & ~(size_t)255;
+}
+
+int surfhip_pack_slab(surfhip_detector* d, const surfhip_point* pts, const float* desc, const int* counts,
+                      int nframes, void* slab)
+{
+    if (!d || !pts || !counts || !slab || nframes < 1) return SURFHIP_ERR_INVALID;
+    const size_t sb = surfhip_slab_bytes(d->max_pts, d->param.nfeatures);
+    HIPCHK(launch_pack(pts, desc, counts, nframes, d->max_pts, d->param.nfeatures, sb, (uint8_t*)slab, d->stream));
+    return SURFHIP_OK;
+}
+
+const char* surfhip_build_info(void)
+{
+    return "libsurfhip gfx950 (" __DATE__ " " __TIME__ ")";
+}
+
+}  // extern "C"

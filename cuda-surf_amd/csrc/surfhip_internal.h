@@ -1,0 +1,74 @@
+// surfhip_internal.h -- parameter blocks and launch helpers shared by the
+// kernel TU (surfhip_kernels.hip) and the C-ABI TU (surfhip_api.hip).
+//
+// The reference keeps these values in process-global __constant__ symbols
+// that every frame re-uploads (surfd.cu:13-24, 27-102; 22 cudaMemcpyToSymbol
+// per frame at 4 octaves).  Here they are computed once per detector and
+// passed by value as kernel arguments, so detectors are independent and a
+// frame costs no host->device parameter traffic.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "surfhip.h"
+
+namespace surfhip {
+
+constexpr int kMaxOct = 8;
+constexpr int kMaxScale = 8;
+constexpr int kSortCap = 16384;     // candidates per frame sorted in LDS
+constexpr int kBandRows = 32;       // integral-image band height
+
+// Per-octave geometry and Hessian/NMS parameters, exactly as the reference
+// host code derives them (surf.cpp:240-292, surfd.cu:2844-2865, 3062-3076).
+struct OctaveParams {
+    int sw, sh, sp, osize;          // response grid (swhp) and plane size
+    long long ooff;                 // float offset of plane 0 in a frame block
+    int octave, delta, init_scale, nscale;
+    int mask[kMaxScale], b1[kMaxScale], x2[kMaxScale], x3[kMaxScale], x4[kMaxScale];
+    float norm[kMaxScale];
+    int borders[kMaxScale];         // host borders[] (d_borders), index s
+    int mb[2];                      // NMS start offsets (maximum_borders)
+    int nms_gx, nms_gy;             // NMS launch extent in threads
+    // previous octave (source of the halfImage planes 0 and 1)
+    int psp, posize;
+    long long pooff;
+};
+
+// Frame-level parameters (SurfParam + integral geometry).
+struct FrameParams {
+    int W, H, ip, iH;               // integral: (W+1) x (H+1), pitch ip ints
+    long long ii_stride;            // ints per frame
+    long long resp_stride;          // floats per frame
+    int max_scale, init_lobe, sampling, noct;
+    float thresh, divisor;
+    int upright, extend, wsz, mag, osz, nfeat;
+};
+
+struct Tables {
+    float lut1[83];
+    float lut2[40];
+    float bins[72];
+};
+
+// ---- launch helpers (defined in surfhip_kernels.hip) -------------------
+hipError_t set_tables(const Tables& t);
+
+hipError_t launch_integral(const uint8_t* frames, int pitch, long long fstride, int nframes,
+                           const FrameParams& P, uint32_t* colsum, int32_t* ii, hipStream_t s);
+hipError_t launch_hessian(const int32_t* ii, float* resp, int nframes, const FrameParams& P,
+                          const OctaveParams& q, int o, hipStream_t s);
+hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,
+                      const OctaveParams& q, int o, surfhip_point* cand, uint32_t* keys,
+                      int* cand_count, int cap, hipStream_t s);
+hipError_t launch_sort(const surfhip_point* cand, const uint32_t* keys, uint64_t* gscratch,
+                       int* cand_count, int cap, int nframes, surfhip_point* out, int max_pts,
+                       int* out_count, int* offsets, int* status, hipStream_t s);
+hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
+                           const int* counts, const int* offsets, int nframes, float* desc,
+                           hipStream_t s);
+hipError_t launch_pack(const surfhip_point* pts, const float* desc, const int* counts, int nframes,
+                       int max_pts, int nfeat, size_t slab_bytes, uint8_t* slab, hipStream_t s);
+
+}  // namespace surfhip

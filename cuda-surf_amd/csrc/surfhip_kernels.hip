@@ -1,0 +1,986 @@
+// surfhip_kernels.hip -- gfx950 kernels of the SURF detect+describe path.
+//
+// Stage map (reference file:line -> kernel here):
+//   integralRow/integralCol   surfd.cu:129-165, 2683-2704  -> k_ii_bandsum, k_ii_bandscan, k_ii_fill
+//   halfImage                 surfd.cu:321-331             -> folded into k_hessian (octaves > 0)
+//   calcHessianMultiConst     surfd.cu:445-481, 2829-2894  -> k_hessian
+//   findMaximumWithInterp     surfd.cu:676-832, 3058-3079  -> k_nms
+//   (atomicInc emission order) surfd.cu:825-830            -> k_sort (canonical order + max_pts cap)
+//   assignOrientationApprox   surfd.cu:1711-1960           -> k_describe<rotated>, phase 1
+//   describe*WithoutNormalization + normalize
+//                             surfd.cu:1566-1615, 2391-2493 -> k_describe, phases 2-3
+//
+// Numerics: this file is compiled with -ffp-contract=off and the pragma
+// below, so each written float operation rounds once (the oracle's
+// semantics); explicit fmaf() only where the reference wrote __fmaf_rn.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "surfhip_internal.h"
+
+namespace surfhip {
+
+#define INV255 0.003921568627f          // surfd.cu:356
+#define H_PI_F 1.5707963267948966f      // cuda_utils.h:8
+#define SEP_ANGLE_F 0.08726646259971647f
+#define WINDOW_F 1.0471975511965976f
+#define M_PI_D 3.14159265358979323846
+
+__constant__ Tables c_tab;
+
+hipError_t set_tables(const Tables& t)
+{
+    return hipMemcpyToSymbol(HIP_SYMBOL(c_tab), &t, sizeof(Tables), 0, hipMemcpyHostToDevice);
+}
+
+__device__ __forceinline__ int f2i_rn(float v) { return (int)__builtin_rintf(v); }
+__device__ __forceinline__ int f2i_rz(float v) { return (int)v; }
+
+__device__ __forceinline__ unsigned lane_id()
+{
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+// ======================================================================
+// Integral image.  Three passes over row bands of kBandRows rows:
+//  (A) k_ii_bandsum : per band, per column, the sum of the band's pixels
+//  (B) k_ii_bandscan: exclusive prefix over bands -> column sums above band
+//  (C) k_ii_fill    : the band's first integral row is the exclusive row
+//      scan of (B); each further row adds the exclusive row scan of the
+//      pixels.  u8 is read twice, the int32 image written once.
+// Semantics of integralRow/integralCol (surfd.cu:129-165): ii[y+1][x+1] is
+// the sum over rows <= y, cols <= x; row 0 / col 0 are 0 (written here).
+// uint32 arithmetic wraps exactly like the reference's int adds.
+// ======================================================================
+
+template <int CPT>
+__device__ __forceinline__ void load_px(const uint8_t* row, int x0, int W, uint32_t (&px)[CPT])
+{
+    if constexpr (CPT == 8) {
+        const uint2 v = *reinterpret_cast<const uint2*>(row + x0);
+        const uint32_t w[2] = {v.x, v.y};
+#pragma unroll
+        for (int k = 0; k < 8; k++) px[k] = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+    } else {
+        const uint4 v = *reinterpret_cast<const uint4*>(row + x0);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 16; k++) px[k] = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+    }
+#pragma unroll
+    for (int k = 0; k < CPT; k++)
+        if (x0 + k >= W) px[k] = 0u;
+}
+
+template <int CPT>
+__global__ __launch_bounds__(256) void k_ii_bandsum(const uint8_t* __restrict__ frames, int pitch,
+                                                    long long fstride, int W, int H, int nbands,
+                                                    uint32_t* __restrict__ colsum, int CW)
+{
+    const int band = blockIdx.x, f = blockIdx.y;
+    const int x0 = threadIdx.x * CPT;
+    if (x0 >= W) return;
+    const int y0 = band * kBandRows;
+    const int rows = min(kBandRows, H - y0);
+    const uint8_t* src = frames + (size_t)f * fstride + (size_t)y0 * pitch;
+    uint32_t acc[CPT];
+#pragma unroll
+    for (int k = 0; k < CPT; k++) acc[k] = 0u;
+    for (int r = 0; r < rows; r++) {
+        uint32_t px[CPT];
+        load_px<CPT>(src + (size_t)r * pitch, x0, W, px);
+#pragma unroll
+        for (int k = 0; k < CPT; k++) acc[k] += px[k];
+    }
+    uint32_t* dst = colsum + ((size_t)f * nbands + band) * CW + x0;
+#pragma unroll
+    for (int k = 0; k < CPT; k += 4)
+        *reinterpret_cast<uint4*>(dst + k) = make_uint4(acc[k], acc[k + 1], acc[k + 2], acc[k + 3]);
+}
+
+__global__ __launch_bounds__(256) void k_ii_bandscan(uint32_t* __restrict__ colsum, int nbands, int CW, int W)
+{
+    const int x = blockIdx.x * 256 + threadIdx.x, f = blockIdx.y;
+    if (x >= W) return;
+    uint32_t* c = colsum + (size_t)f * nbands * CW + x;
+    uint32_t run = 0u;
+    for (int b = 0; b < nbands; b++) {
+        const uint32_t v = c[(size_t)b * CW];
+        c[(size_t)b * CW] = run;
+        run += v;
+    }
+}
+
+// Exclusive scan across the 256-thread block of CPT consecutive values per
+// thread (wave64 shuffle scan + LDS exchange of the 4 wave totals).
+template <int CPT>
+__device__ __forceinline__ void block_excl_scan(uint32_t (&v)[CPT], uint32_t* lds4)
+{
+    uint32_t run = 0u;
+#pragma unroll
+    for (int k = 0; k < CPT; k++) {
+        const uint32_t t = v[k];
+        v[k] = run;
+        run += t;
+    }
+    const unsigned lane = lane_id();
+    const int wave = threadIdx.x >> 6;
+    uint32_t inc = run;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t n = (uint32_t)__shfl_up((int)inc, d, 64);
+        if (lane >= (unsigned)d) inc += n;
+    }
+    if (lane == 63) lds4[wave] = inc;
+    __syncthreads();
+    uint32_t base = inc - run;
+    for (int w = 0; w < wave; w++) base += lds4[w];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < CPT; k++) v[k] += base;
+}
+
+template <int CPT>
+__global__ __launch_bounds__(256) void k_ii_fill(const uint8_t* __restrict__ frames, int pitch,
+                                                 long long fstride, int W, int H, int nbands,
+                                                 const uint32_t* __restrict__ colpre, int CW,
+                                                 int32_t* __restrict__ ii, int ip, long long istride)
+{
+    __shared__ uint32_t lds4[4];
+    const int band = blockIdx.x, f = blockIdx.y;
+    const int x0 = threadIdx.x * CPT;
+    const bool active = x0 <= W;               // thread owns integral columns x0..x0+CPT-1
+    const int y0 = band * kBandRows;
+    const int rows = min(kBandRows, H - y0);
+    uint32_t acc[CPT];
+    {
+        const uint32_t* c = colpre + ((size_t)f * nbands + band) * CW;
+#pragma unroll
+        for (int k = 0; k < CPT; k++) acc[k] = (x0 + k < W) ? c[x0 + k] : 0u;
+    }
+    block_excl_scan<CPT>(acc, lds4);           // acc = ii[y0][x0 + k]
+    uint32_t* out = reinterpret_cast<uint32_t*>(ii) + (size_t)f * istride;
+    if (band == 0 && active) {
+#pragma unroll
+        for (int k = 0; k < CPT; k += 4)
+            *reinterpret_cast<uint4*>(out + x0 + k) = make_uint4(0u, 0u, 0u, 0u);
+    }
+    const uint8_t* src = frames + (size_t)f * fstride + (size_t)y0 * pitch;
+    for (int r = 0; r < rows; r++) {
+        uint32_t px[CPT];
+        if (x0 < W) load_px<CPT>(src + (size_t)r * pitch, x0, W, px);
+        else {
+#pragma unroll
+            for (int k = 0; k < CPT; k++) px[k] = 0u;
+        }
+        block_excl_scan<CPT>(px, lds4);
+#pragma unroll
+        for (int k = 0; k < CPT; k++) acc[k] += px[k];
+        if (active) {
+            uint32_t* dst = out + (size_t)(y0 + r + 1) * ip + x0;
+#pragma unroll
+            for (int k = 0; k < CPT; k += 4)
+                *reinterpret_cast<uint4*>(dst + k) = make_uint4(acc[k], acc[k + 1], acc[k + 2], acc[k + 3]);
+        }
+    }
+}
+
+hipError_t launch_integral(const uint8_t* frames, int pitch, long long fstride, int nframes,
+                           const FrameParams& P, uint32_t* colsum, int32_t* ii, hipStream_t s)
+{
+    const int nbands = (P.H + kBandRows - 1) / kBandRows;
+    const int W = P.W;
+    dim3 grid(nbands, nframes);
+    if (W + 1 <= 2048) {
+        const int CW = 2048;
+        k_ii_bandsum<8><<<grid, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW);
+        k_ii_bandscan<<<dim3((W + 255) / 256, nframes), 256, 0, s>>>(colsum, nbands, CW, W);
+        k_ii_fill<8><<<grid, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW, ii, P.ip, P.ii_stride);
+    } else if (W + 1 <= 4096) {
+        const int CW = 4096;
+        k_ii_bandsum<16><<<grid, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW);
+        k_ii_bandscan<<<dim3((W + 255) / 256, nframes), 256, 0, s>>>(colsum, nbands, CW, W);
+        k_ii_fill<16><<<grid, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW, ii, P.ip, P.ii_stride);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ======================================================================
+// Hessian determinant (calcHessianMultiConst, surfd.cu:445-481; getHessian
+// surfd.cu:353-366).  One thread per response sample of one octave, all
+// scales of the octave; cells outside a scale's valid window are written 0
+// (the reference's cudaMemset, surf.cpp:348).  For octaves > 0 the same
+// thread also writes planes 0/1 from the previous octave's planes 2/4
+// (halfImage, surfd.cu:321-331).
+// ======================================================================
+
+// getSum (surfd.cu:334-343): inclusive rect [x2..x1] x [y2..y1].
+__device__ __forceinline__ uint32_t box(const uint32_t* __restrict__ I, int ip, int x1, int y1, int x2, int y2)
+{
+    const int yp1 = (y1 + 1) * ip;
+    const int yp2 = y2 * ip;
+    return I[yp1 + x1 + 1] + I[yp2 + x2] - I[yp2 + x1 + 1] - I[yp1 + x2];
+}
+
+__device__ __forceinline__ float hessian_at(const uint32_t* __restrict__ I, int ip, int x0, int y0,
+                                            int m, int x2, int x3, int x4)
+{
+    const int xp = x0 + m, xm = x0 - m, yp = y0 + m, ym = y0 - m;
+    const int32_t sxx = (int32_t)(box(I, ip, xp + x2, y0 + x3, xm - x2, y0 - x3)
+                                  - 3u * box(I, ip, x0 + x2, y0 + x3, x0 - x2, y0 - x3));
+    const int32_t syy = (int32_t)(box(I, ip, x0 + x3, yp + x2, x0 - x3, ym - x2)
+                                  - 3u * box(I, ip, x0 + x3, y0 + x2, x0 - x3, y0 - x2));
+    const int32_t sxy = (int32_t)(box(I, ip, x0 + x4, y0, x0, y0 - x4)
+                                  + box(I, ip, x0, y0 + x4, x0 - x4, y0)
+                                  - box(I, ip, x0 + x4, y0 + x4, x0, y0)
+                                  - box(I, ip, x0, y0, x0 - x4, y0 - x4));
+    const float rr = INV255 * INV255;
+    const float dxx = (float)sxx;
+    const float dyy = (float)syy;
+    const float dxy = 0.6f * (float)sxy;
+    const float a = dxx * dyy;
+    const float b = dxy * dxy;
+    return rr * (a - b);
+}
+
+template <int NS>
+__global__ __launch_bounds__(256) void k_hessian(const int32_t* __restrict__ ii, float* __restrict__ resp,
+                                                 FrameParams P, OctaveParams q, int with_half)
+{
+    const int ix = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int iy = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int f = blockIdx.z;
+    if (ix >= q.sw || iy >= q.sh) return;
+    const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
+    float* F = resp + (size_t)f * P.resp_stride;
+    float* R = F + q.ooff + (size_t)iy * q.sp + ix;
+    const int x0 = q.delta * ix, y0 = q.delta * iy;
+#pragma unroll
+    for (int i = 0; i < NS; i++) {
+        const int b1 = q.b1[i];
+        float v = 0.f;
+        if (ix >= b1 && ix < q.sw - b1 && iy >= b1 && iy < q.sh - b1)
+            v = hessian_at(I, P.ip, x0, y0, q.mask[i], q.x2[i], q.x3[i], q.x4[i]) * q.norm[i];
+        R[(size_t)(q.init_scale + i) * q.osize] = v;
+    }
+    if (with_half) {
+        const float* src = F + q.pooff + (size_t)(2 * iy) * q.psp + 2 * ix;
+        R[0] = src[(size_t)2 * q.posize];
+        R[(size_t)q.osize] = src[(size_t)4 * q.posize];
+    }
+}
+
+hipError_t launch_hessian(const int32_t* ii, float* resp, int nframes, const FrameParams& P,
+                          const OctaveParams& q, int o, hipStream_t s)
+{
+    dim3 grid((q.sw + 63) / 64, (q.sh + 3) / 4, nframes);
+    if (q.nscale == 5) k_hessian<5><<<grid, 256, 0, s>>>(ii, resp, P, q, o > 0);
+    else if (q.nscale == 3) k_hessian<3><<<grid, 256, 0, s>>>(ii, resp, P, q, o > 0);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+// ======================================================================
+// Scale-space NMS + interpolation + makePoint (findMaximumWithInterp,
+// surfd.cu:676-832; fitQuadrat 942-988; solveLinearSystem 835-887;
+// makePoint 1001-1022).  One thread per 2x2 block of one NMS level.
+// Survivors are compacted per wave (ballot + one atomic per wave) into the
+// frame's candidate buffer with a canonical key (octave, level, row, col);
+// k_sort restores that order, so the output is deterministic.
+// ======================================================================
+
+__device__ void solve3(float* sol, float (&sq)[3][3])
+{
+    int row, col, c, pivot = 0, i;
+    float maxc, coef, temp, mult, val;
+    for (col = 0; col < 2; col++) {
+        maxc = -1.f;
+        for (row = col; row < 3; row++) {
+            coef = sq[row][col];
+            coef = (coef < 0.f ? -coef : coef);
+            if (coef > maxc) { maxc = coef; pivot = row; }
+        }
+        if (pivot != col) {
+            for (i = 0; i < 3; i++) { temp = sq[pivot][i]; sq[pivot][i] = sq[col][i]; sq[col][i] = temp; }
+            temp = sol[pivot]; sol[pivot] = sol[col]; sol[col] = temp;
+        }
+        for (row = col + 1; row < 3; row++) {
+            mult = sq[row][col] / sq[col][col];
+            for (c = col; c < 3; c++) sq[row][c] = sq[row][c] - mult * sq[col][c];
+            sol[row] = sol[row] - mult * sol[col];
+        }
+    }
+    for (row = 2; row >= 0; row--) {
+        val = sol[row];
+        for (col = 2; col > row; col--) val = val - sol[col] * sq[row][col];
+        sol[row] = val / sq[row][row];
+    }
+}
+
+__device__ float fit_quad(const float* __restrict__ src, float (&off)[3], int s, int r, int c, int osize, int sp)
+{
+    const float* cur = src + (size_t)s * osize;
+    const float* prv = cur - osize;
+    const float* nxt = cur + osize;
+    const int idx = r * sp + c;
+    const int inr = idx + sp, ipr = idx - sp, inc = idx + 1, ipc = idx - 1;
+    float g[3], H[3][3];
+    g[0] = (nxt[idx] - prv[idx]) * 0.5f;
+    g[1] = (cur[inr] - cur[ipr]) * 0.5f;
+    g[2] = (cur[inc] - cur[ipc]) * 0.5f;
+    const float temp = cur[idx] + cur[idx];
+    H[0][0] = (prv[idx] + nxt[idx]) - temp;
+    H[1][1] = (cur[inr] + cur[ipr]) - temp;
+    H[2][2] = (cur[inc] + cur[ipc]) - temp;
+    H[0][1] = ((nxt[inr] - nxt[ipr]) - (prv[inr] - prv[ipr])) * 0.25f;
+    H[0][2] = ((nxt[inc] - nxt[ipc]) - (prv[inc] - prv[ipc])) * 0.25f;
+    H[1][2] = ((cur[inr + 1] - cur[inr - 1]) - (cur[ipr + 1] - cur[ipr - 1])) * 0.25f;
+    H[1][0] = H[0][1];
+    H[2][0] = H[0][2];
+    H[2][1] = H[1][2];
+    off[0] = -g[0];
+    off[1] = -g[1];
+    off[2] = -g[2];
+    solve3(off, H);
+    const float dot = (off[0] * g[0] + off[1] * g[1]) + off[2] * g[2];
+    return cur[idx] + 0.5f * dot;
+}
+
+__device__ __forceinline__ int32_t trace_sign(const uint32_t* __restrict__ I, int ip, const int* v)
+{
+    const int32_t lxx = (int32_t)(box(I, ip, v[5] + v[2], v[1] + v[3], v[6] - v[2], v[1] - v[3])
+                                  - 3u * box(I, ip, v[0] + v[2], v[1] + v[3], v[0] - v[2], v[1] - v[3]));
+    const int32_t lyy = (int32_t)(box(I, ip, v[0] + v[3], v[7] + v[2], v[0] - v[3], v[8] - v[2])
+                                  - 3u * box(I, ip, v[0] + v[3], v[1] + v[2], v[0] - v[3], v[1] - v[2]));
+    return ((int32_t)((uint32_t)lxx + (uint32_t)lyy) > 0) ? 1 : -1;
+}
+
+__device__ bool nms_point(const uint32_t* __restrict__ I, const float* __restrict__ src, const FrameParams& P,
+                          const OctaveParams& q, int o, int z, int x, int y, surfhip_point& pt)
+{
+    const int sw = q.sw, sh = q.sh, sp = q.sp, osize = q.osize;
+    const int k = 2 * z + 1;
+    const int mb = q.mb[z];
+    const int i = mb + y * 2;
+    const int j = mb + x * 2;
+    if (i >= sh - mb || j >= sw - mb) return false;
+
+    int iw = i * sp + j, ix = iw + 1, iy = iw + sp, iz = iy + 1;
+    const float* cs = src + (size_t)k * osize;
+    int cas = 0;
+    float best = cs[iw];
+    if (cs[ix] > best) { best = cs[ix]; cas = 1; }
+    if (cs[iy] > best) { best = cs[iy]; cas = 2; }
+    if (cs[iz] > best) { best = cs[iz]; cas = 3; }
+    cs += osize;
+    if (cs[iw] > best) { best = cs[iw]; cas = 4; }
+    if (cs[ix] > best) { best = cs[ix]; cas = 5; }
+    if (cs[iy] > best) { best = cs[iy]; cas = 6; }
+    if (cs[iz] > best) { best = cs[iz]; cas = 7; }
+    if (best < P.thresh * 0.8f || (k + 1 == P.max_scale - 1 && cas > 3)) return false;
+
+    int s = k, r = i, c = j, ds = -1, dr = -1, dc = -1;
+    if (cas != 0) {
+        if (cas == 1) { c = j + 1; dc = 1; }
+        else if (cas == 2) { r = i + 1; dr = 1; }
+        else if (cas == 3) { c = j + 1; r = i + 1; dc = 1; dr = 1; }
+        else {
+            s++; ds = 1;
+            if (cas == 5) { c = j + 1; dc = 1; }
+            else if (cas == 6) { r = i + 1; dr = 1; }
+            else if (cas == 7) { c = j + 1; r = i + 1; dc = 1; dr = 1; }
+        }
+    }
+    int ss = s + ds;
+    cs = src + (size_t)ss * osize;
+    iy = (r - dr) * sp + c; ix = iy - 1; iz = iy + 1;
+    if (best < cs[ix] || best < cs[iy] || best < cs[iz]) return false;
+    iy += dr * sp; ix = iy - 1; iz = iy + 1;
+    if (best < cs[ix] || best < cs[iy] || best < cs[iz]) return false;
+    iy += dr * sp; ix = iy - 1; iz = iy + 1;
+    if (best < cs[ix] || best < cs[iy] || best < cs[iz]) return false;
+    cs = src + (size_t)s * osize;
+    if (best < cs[ix] || best < cs[iy] || best < cs[iz]) return false;
+    iw = r * sp + c + dc;
+    if (best < cs[iw]) return false;
+    iw -= dr * sp;
+    if (best < cs[iw]) return false;
+    ss = s - ds;
+    cs = src + (size_t)ss * osize;
+    if (best < cs[ix] || best < cs[iy] || best < cs[iz] || best < cs[iw]) return false;
+    iw += dr * sp;
+    if (best < cs[iw]) return false;
+
+    float off[3] = {0.f, 0.f, 0.f};
+    float strength = 0.f;
+    int newr = r, newc = c;
+    for (int mv = 0; mv < 5; mv++) {
+        r = newr; c = newc;
+        strength = fit_quad(src, off, s, r, c, osize, sp);
+        const int bs = q.borders[s];
+        if (off[1] > 0.6f && r < sh - bs) newr++;
+        if (off[1] < -0.6f && r > bs) newr--;
+        if (off[2] > 0.6f && c < sw - bs) newc++;
+        if (off[2] < -0.6f && c > bs) newc--;
+        if (newr == r && newc == c) break;
+    }
+    if (__builtin_isnan(off[0]) || __builtin_isnan(off[1]) || __builtin_isnan(off[2]) ||
+        fabsf(off[0]) > 1.5f || fabsf(off[1]) > 1.5f || fabsf(off[2]) > 1.5f || strength < P.thresh)
+        return false;
+
+    const int octave = q.octave;
+    const float t2 = (((float)s + off[0]) * 2.f) * (float)octave;
+    const float ns = ((float)(P.init_lobe + (octave - 1) * P.max_scale) + t2) / 3.f;
+    const float ny = (float)octave * ((float)r + off[1]);
+    const float nx = (float)octave * ((float)c + off[2]);
+    const float temp_delta = (float)P.sampling * P.divisor;
+    pt.x = nx * temp_delta;
+    pt.y = ny * temp_delta;
+    pt.scale = (1.2f * ns) * P.divisor;
+    pt.o = o;
+    pt.strength = strength;
+    pt.ori = 0.f;
+    pt.score = 0.f;
+    pt.match = -1;
+    pt.match_x = 0.f;
+    pt.match_y = 0.f;
+    pt.ambiguity = 0.f;
+    int v[9];
+    const int temp = f2i_rz(fmaf(3.f, ns, 0.5f));
+    v[0] = f2i_rz(fmaf(nx, (float)P.sampling, 0.5f));
+    v[1] = f2i_rz(fmaf(ny, (float)P.sampling, 0.5f));
+    v[2] = temp / 2;
+    v[3] = v[2] + v[2];
+    v[4] = v[2] + v[3];
+    v[5] = v[0] + temp;
+    v[6] = v[0] - temp;
+    v[7] = v[1] + temp;
+    v[8] = v[1] - temp;
+    pt.laplace = trace_sign(I, P.ip, v);
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_nms(const int32_t* __restrict__ ii, const float* __restrict__ resp,
+                                             FrameParams P, OctaveParams q, int o,
+                                             surfhip_point* __restrict__ cand, uint32_t* __restrict__ keys,
+                                             int* __restrict__ cand_count, int cap)
+{
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int f = blockIdx.z >> 1, z = blockIdx.z & 1;
+    const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
+    const float* src = resp + (size_t)f * P.resp_stride + q.ooff;
+    surfhip_point pt;
+    bool ok = false;
+    if (x < q.nms_gx && y < q.nms_gy) ok = nms_point(I, src, P, q, o, z, x, y, pt);
+    const unsigned long long m = __ballot(ok);
+    if (m == 0ull) return;
+    const int leader = __builtin_ctzll(m);
+    const unsigned lane = lane_id();
+    int base = 0;
+    if ((int)lane == leader) base = atomicAdd(&cand_count[f], (int)__popcll(m));
+    base = __shfl(base, leader, 64);
+    if (ok) {
+        const int slot = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+        if (slot < cap) {
+            cand[(size_t)f * cap + slot] = pt;
+            keys[(size_t)f * cap + slot] = ((uint32_t)o << 29) | ((uint32_t)z << 28) |
+                                           ((uint32_t)y << 14) | (uint32_t)x;
+        }
+    }
+}
+
+hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,
+                      const OctaveParams& q, int o, surfhip_point* cand, uint32_t* keys,
+                      int* cand_count, int cap, hipStream_t s)
+{
+    if (q.nms_gx <= 0 || q.nms_gy <= 0) return hipSuccess;
+    if (q.nms_gx >= (1 << 14) || q.nms_gy >= (1 << 14)) return hipErrorInvalidValue;
+    dim3 grid((q.nms_gx + 63) / 64, (q.nms_gy + 3) / 4, nframes * 2);
+    k_nms<<<grid, 256, 0, s>>>(ii, resp, P, q, o, cand, keys, cand_count, cap);
+    return hipGetLastError();
+}
+
+// ======================================================================
+// Canonical order + max_pts cap.  The reference emits in atomicInc order
+// and can write past max_pts (surfd.cu:827-830, no pi<max guard); here each
+// frame's candidates are sorted by key (bitonic, in LDS up to kSortCap, in
+// a global scratch beyond) and the first max_pts are kept.
+// ======================================================================
+
+template <typename PtrT>
+__device__ void bitonic_sort(PtrT s, int n)
+{
+    for (int k = 2; k <= n; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < n; i += blockDim.x) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const uint64_t a = s[i], b = s[ixj];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) { s[i] = b; s[ixj] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_sort(const surfhip_point* __restrict__ cand,
+                                               const uint32_t* __restrict__ keys,
+                                               uint64_t* __restrict__ gscratch, int* cand_count, int cap,
+                                               surfhip_point* __restrict__ out, int max_pts,
+                                               int* __restrict__ out_count, int* status)
+{
+    extern __shared__ __attribute__((aligned(16))) uint64_t sk[];
+    const int f = blockIdx.x;
+    int cnt = cand_count[f];
+    if (cnt > cap) {
+        if (threadIdx.x == 0) atomicOr(status, 1);
+        cnt = cap;
+    }
+    int n = 1;
+    while (n < cnt) n <<= 1;
+    const bool in_lds = n <= kSortCap;
+    uint64_t* s = in_lds ? sk : gscratch + (size_t)f * cap;
+    if (!in_lds && n > cap) {          // gscratch holds cap entries per frame
+        if (threadIdx.x == 0) atomicOr(status, 2);
+        return;
+    }
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        s[i] = (i < cnt) ? (((uint64_t)keys[(size_t)f * cap + i] << 32) | (uint32_t)i) : ~0ull;
+    __syncthreads();
+    bitonic_sort(s, n);
+    const int keep = min(cnt, max_pts);
+    for (int t = threadIdx.x; t < keep; t += blockDim.x)
+        out[(size_t)f * max_pts + t] = cand[(size_t)f * cap + (uint32_t)(s[t] & 0xffffffffu)];
+    if (threadIdx.x == 0) out_count[f] = keep;
+}
+
+__global__ __launch_bounds__(1024) void k_offsets(const int* __restrict__ counts, int nframes, int* __restrict__ offsets)
+{
+    __shared__ int part[1024];
+    const int per = (nframes + 1023) / 1024;
+    const int b = threadIdx.x * per;
+    int sum = 0;
+    for (int i = 0; i < per; i++) if (b + i < nframes) sum += counts[b + i];
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int run = 0;
+        for (int t = 0; t < 1024; t++) { const int v = part[t]; part[t] = run; run += v; }
+        offsets[nframes] = run;
+    }
+    __syncthreads();
+    int run = part[threadIdx.x];
+    for (int i = 0; i < per; i++)
+        if (b + i < nframes) { offsets[b + i] = run; run += counts[b + i]; }
+}
+
+hipError_t launch_sort(const surfhip_point* cand, const uint32_t* keys, uint64_t* gscratch,
+                       int* cand_count, int cap, int nframes, surfhip_point* out, int max_pts,
+                       int* out_count, int* offsets, int* status, hipStream_t s)
+{
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)(kSortCap * sizeof(uint64_t)));
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    k_sort<<<nframes, 1024, kSortCap * sizeof(uint64_t), s>>>(cand, keys, gscratch, cand_count, cap, out,
+                                                              max_pts, out_count, status);
+    k_offsets<<<1, 1024, 0, s>>>(out_count, nframes, offsets);
+    return hipGetLastError();
+}
+
+// ======================================================================
+// Orientation + descriptor + normalize, one wave (64 lanes) per keypoint,
+// 4 keypoints per 256-thread workgroup, grid-strided over all keypoints of
+// the batch.  Haar responses are gathered from the integral image (L1/L2);
+// descriptor bins accumulate with LDS float atomics (order-free, like the
+// reference's global atomics, surfd.cu:1222-1266); the orientation
+// histogram is reduced in fixed sample order so `ori` is reproducible.
+// ======================================================================
+
+__device__ __forceinline__ int32_t wavelet1(const uint32_t* __restrict__ I, int ip, int x, int y, int size)
+{
+    return (int32_t)(box(I, ip, x + size, y, x - size, y - size) - box(I, ip, x + size, y + size, x - size, y));
+}
+__device__ __forceinline__ int32_t wavelet2(const uint32_t* __restrict__ I, int ip, int x, int y, int size)
+{
+    return (int32_t)(box(I, ip, x + size, y + size, x, y - size) - box(I, ip, x, y + size, x - size, y - size));
+}
+
+// dFastAtan2 (surfd.cu:114-126)
+__device__ __forceinline__ float fast_atan2(float y, float x)
+{
+    const float absx = fabsf(x), absy = fabsf(y);
+    const float a = fminf(absx, absy) / fmaxf(absx, absy);
+    const float s = a * a;
+    float r = fmaf(fmaf(fmaf(-0.0464964749f, s, 0.15931422f), s, -0.327622764f), s * a, a);
+    r = (absy > absx ? H_PI_F - r : r);
+    r = (x < 0 ? (float)(M_PI_D - (double)r) : r);
+    r = (y < 0 ? -r : r);
+    return r;
+}
+
+// Deterministic sin/cos standing in for __sinf/__cosf (surfd.cu:2423-2424);
+// identical operation sequence to the oracle's or_sinf/or_cosf.
+__device__ __forceinline__ float sincos_poly(float x, int want_cos)
+{
+    const float q = x * 0.636619772f;
+    const float kf = __builtin_rintf(q);
+    int k = (int)kf;
+    const float r = ((x - kf * 1.5703125f) - kf * 4.837512969970703125e-4f) - kf * 7.54978995489188216e-8f;
+    const float z = r * r;
+    float ps = -1.9515295891e-4f * z;
+    ps = ps + 8.3321608736e-3f;
+    ps = ps * z;
+    ps = ps - 1.6666654611e-1f;
+    ps = ps * z;
+    ps = ps * r;
+    const float sn = ps + r;
+    float pc = 2.443315711809948e-5f * z;
+    pc = pc - 1.388731625493765e-3f;
+    pc = pc * z;
+    pc = pc + 4.166664568298827e-2f;
+    pc = pc * z;
+    pc = pc * z;
+    const float cs = (pc - 0.5f * z) + 1.0f;
+    k += want_cos;
+    switch (k & 3) {
+        case 0: return sn;
+        case 1: return cs;
+        case 2: return -sn;
+        default: return -cs;
+    }
+}
+
+// placeInIndex (surfd.cu:1199-1271) into an LDS descriptor.
+__device__ __forceinline__ void place(float* d, int wsz, int osz, float mag1, int ori1, float mag2, int ori2,
+                                      float rx, float cx)
+{
+    const int ri = f2i_rz(rx >= 0.f ? rx : rx - 1.f);
+    const int ci = f2i_rz(cx >= 0.f ? cx : cx - 1.f);
+    const float rfrac = rx - (float)ri;
+    const float cfrac = cx - (float)ci;
+    const float cfrac1 = 1 - cfrac;
+    if (ri >= 0) {
+        const float rw1 = mag1 * (1.f - rfrac), rw2 = mag2 * (1.f - rfrac);
+        if (ci >= 0) {
+            const int o0 = ri * wsz * osz + ci * osz;
+            atomicAdd(&d[o0 + ori1], rw1 * cfrac1);
+            atomicAdd(&d[o0 + ori2], rw2 * cfrac1);
+        }
+        if (ci + 1 < wsz) {
+            const int o0 = ri * wsz * osz + (ci + 1) * osz;
+            atomicAdd(&d[o0 + ori1], rw1 * cfrac);
+            atomicAdd(&d[o0 + ori2], rw2 * cfrac);
+        }
+    }
+    if (ri + 1 < wsz) {
+        const float rw1 = mag1 * rfrac, rw2 = mag2 * rfrac;
+        if (ci >= 0) {
+            const int o0 = (ri + 1) * wsz * osz + ci * osz;
+            atomicAdd(&d[o0 + ori1], rw1 * cfrac1);
+            atomicAdd(&d[o0 + ori2], rw2 * cfrac1);
+        }
+        if (ci + 1 < wsz) {
+            const int o0 = (ri + 1) * wsz * osz + (ci + 1) * osz;
+            atomicAdd(&d[o0 + ori1], rw1 * cfrac);
+            atomicAdd(&d[o0 + ori2], rw2 * cfrac);
+        }
+    }
+}
+
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct OriScratch {
+    int   hid[361];
+    float ang[361];
+    float psum[361];
+    int   hist[72];
+    float avg[72];
+    float part[72];
+    float pas[84];
+    float ws[72];
+    float was[72];
+};
+
+// assignOrientationApprox (surfd.cu:1711-1960) for one keypoint on one wave.
+__device__ float orientation_wave(const uint32_t* __restrict__ I, const FrameParams& P, const surfhip_point& p,
+                                  OriScratch& S, unsigned lane)
+{
+    const int ip = P.ip;
+    const float scale = p.scale;
+    const int pixsi = f2i_rz(2.f * scale + 1.6f);
+    const int pixsi2 = f2i_rz(scale + 0.8f);
+    const int ixo = f2i_rn(p.x), iyo = f2i_rn(p.y);
+    for (int t = lane; t < 361; t += 64) {
+        const int y1 = t / 19 - 9, x1 = t % 19 - 9;
+        const int xx = ixo + x1 * pixsi2, yy = iyo + y1 * pixsi2;
+        int hid = -1;
+        float angle = 0.f, psum = 0.f;
+        if (yy + pixsi + 2 < P.iH && yy - pixsi > -1 && xx + pixsi + 2 < P.W + 1 && xx - pixsi > -1) {
+            const int distsq = y1 * y1 + x1 * x1;
+            if ((float)distsq < 81.5f) {
+                const float dx = (float)wavelet2(I, ip, xx, yy, pixsi) * INV255;
+                const float dy = (float)wavelet1(I, ip, xx, yy, pixsi) * INV255;
+                const float mag = sqrtf(dx * dx + dy * dy);
+                if (mag > 0.f) {
+                    angle = fast_atan2(dy, dx);
+                    hid = f2i_rz((float)(((double)angle + M_PI_D) / (double)SEP_ANGLE_F)) % 72;
+                    psum = c_tab.lut1[distsq] * mag;
+                }
+            }
+        }
+        S.hid[t] = hid;
+        S.ang[t] = angle;
+        S.psum[t] = psum;
+    }
+    wave_sync();
+    // per-bin sums in row-major sample order
+    for (int b = lane; b < 72; b += 64) {
+        int cnt = 0;
+        float sa = 0.f, sp = 0.f, spa = 0.f, swrap = 0.f;
+        for (int t = 0; t < 361; t++) {
+            if (S.hid[t] == b) {
+                const float a = S.ang[t], w = S.psum[t];
+                cnt += 1;
+                sa = sa + a;
+                sp = sp + w;
+                spa = spa + a * w;
+                if (b < 6) swrap = swrap + (float)(((double)a + 2 * M_PI_D) * (double)w);
+                else if (b >= 66) swrap = swrap + (float)(((double)a - 2 * M_PI_D) * (double)w);
+            }
+        }
+        S.hist[b] = cnt;
+        S.avg[b] = cnt > 0 ? sa / (float)cnt : c_tab.bins[b];
+        S.part[b] = sp;
+        S.pas[b + 6] = spa;
+        if (b < 6) S.pas[b + 78] = swrap;
+        else if (b >= 66) S.pas[b - 66] = swrap;
+    }
+    wave_sync();
+    for (int i = lane; i < 72; i += 64) {
+        float ws = 0.f, was = 0.f;
+        for (int j = -6; j <= 6; j++) {
+            int k = i + j;
+            if (j == -6) {
+                float residual;
+                if (k < 0) {
+                    k += 72;
+                    const int k1 = (k + 1) % 72;
+                    const float t = (c_tab.bins[k1] + (WINDOW_F / 2)) - S.avg[i];
+                    residual = (float)((double)t - (c_tab.bins[k1] < 0 ? 0.0 : 2 * M_PI_D));
+                } else {
+                    residual = (c_tab.bins[k + 1] + (WINDOW_F / 2)) - S.avg[i];
+                }
+                const float er = residual / SEP_ANGLE_F;
+                ws = ws + er * S.part[k];
+                was = was + er * S.pas[i];
+            } else if (j == 6) {
+                float residual;
+                if (k >= 72) {
+                    k -= 72;
+                    const float t = S.avg[i] + (WINDOW_F / 2);
+                    residual = (float)(((double)t - 2 * M_PI_D) - (double)c_tab.bins[k]);
+                } else {
+                    residual = (S.avg[i] + (WINDOW_F / 2)) - c_tab.bins[k];
+                }
+                const float er = residual / SEP_ANGLE_F;
+                ws = ws + er * S.part[k];
+                was = was + er * S.pas[i + 12];
+            } else {
+                was = was + S.pas[k + 6];
+                if (k < 0) k += 72;
+                else if (k >= 72) k -= 72;
+                ws = ws + S.part[k];
+            }
+        }
+        S.ws[i] = ws;
+        S.was[i] = was;
+    }
+    wave_sync();
+    float ori = 0.f;
+    if (lane == 0) {
+        // tree argmax in chunks of 64 and 8, strict '<' (surfd.cu:1921-1947)
+        for (int stride = 32; stride > 0; stride >>= 1)
+            for (int t = 0; t < stride; t++)
+                if (S.ws[t] < S.ws[t + stride]) { S.ws[t] = S.ws[t + stride]; S.was[t] = S.was[t + stride]; }
+        for (int stride = 4; stride > 0; stride >>= 1)
+            for (int t = 0; t < stride; t++)
+                if (S.ws[64 + t] < S.ws[64 + t + stride]) { S.ws[64 + t] = S.ws[64 + t + stride]; S.was[64 + t] = S.was[64 + t + stride]; }
+        float w0 = S.ws[0], a0 = S.was[0];
+        if (w0 < S.ws[64]) { w0 = S.ws[64]; a0 = S.was[64]; }
+        ori = a0 / w0;
+    }
+    ori = __shfl(ori, 0, 64);
+    wave_sync();
+    return ori;
+}
+
+template <bool UPRIGHT>
+__global__ __launch_bounds__(256) void k_describe(const int32_t* __restrict__ ii, FrameParams P,
+                                                  surfhip_point* __restrict__ pts, int max_pts,
+                                                  const int* __restrict__ counts, const int* __restrict__ offsets,
+                                                  int nframes, float* __restrict__ desc)
+{
+    __shared__ float sdesc[4][128];
+    __shared__ OriScratch sori[UPRIGHT ? 1 : 4];
+    const unsigned lane = lane_id();
+    const int w = threadIdx.x >> 6;
+    const int total = offsets[nframes];
+    const int nf = P.nfeat, wsz = P.wsz, osz = P.osz;
+    const float fw = (float)wsz;
+    const float wofs = (float)wsz * 0.5f - 0.5f;
+    float* d = sdesc[w];
+    for (int g = blockIdx.x * 4 + w; g < total; g += gridDim.x * 4) {
+        int lo = 0, hi = nframes;            // offsets[lo] <= g < offsets[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (offsets[mid] <= g) lo = mid; else hi = mid;
+        }
+        const int f = lo, i = g - offsets[lo];
+        surfhip_point* pp = pts + (size_t)f * max_pts + i;
+        const surfhip_point p = *pp;
+        const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
+        const int ip = P.ip;
+        float ori = 0.f;
+        if constexpr (!UPRIGHT) {
+            ori = orientation_wave(I, P, p, sori[w], lane);
+            if (lane == 0) pp->ori = ori;
+        }
+        for (int t = lane; t < nf; t += 64) d[t] = 0.f;
+        wave_sync();
+        const float scale = 1.65f * p.scale;
+        const int step = max(f2i_rn(scale * 0.5f), 1);
+        const int ix = f2i_rn(p.x), iy = f2i_rn(p.y);
+        const float spacing = scale * (float)P.mag;
+        const int hs = f2i_rz(scale);
+        const int rlim = P.iH - 1 - hs, clim = P.W - hs;   // whps[1].y-1-s, whps[1].x-1-s
+        if constexpr (UPRIGHT) {
+            const float dx0 = p.x - (float)ix, dy0 = p.y - (float)iy;
+            const int iradius = f2i_rn(((spacing * (float)(wsz + 1)) * 0.5f) / (float)step);
+            const int side = 2 * iradius + 1;
+            const int nsamp = side * side;
+            for (int t = lane; t < nsamp; t += 64) {
+                const int si = t / side - iradius, sj = t % side - iradius;
+                const float rpos = ((float)(step * si) - dy0) / spacing;
+                const float cpos = ((float)(step * sj) - dx0) / spacing;
+                const float rx = rpos + wofs, cx = cpos + wofs;
+                if (!(rx > -1.f && rx < fw && cx > -1.f && cx < fw)) continue;
+                const int r = iy + si * step, c = ix + sj * step;
+                if (!(r >= 1 + hs && r < rlim && c >= 1 + hs && c < clim)) continue;
+                const float weight = c_tab.lut2[f2i_rz(rpos * rpos + cpos * cpos)];
+                const float dx = (weight * (float)wavelet2(I, ip, c, r, hs)) * INV255;
+                const float dy = (weight * (float)wavelet1(I, ip, c, r, hs)) * INV255;
+                if (!P.extend) {
+                    place(d, wsz, osz, dx, (dx < 0 ? 0 : 1), dy, (dy < 0 ? 2 : 3), rx, cx);
+                } else {
+                    place(d, wsz, osz, dx, (dy < 0 ? 0 : 1), fabsf(dx), (dy < 0 ? 2 : 3), rx, cx);
+                    place(d, wsz, osz, dy, (dx < 0 ? 4 : 5), fabsf(dy), (dx < 0 ? 6 : 7), rx, cx);
+                }
+            }
+        } else {
+            const float fracx = p.x - (float)ix, fracy = p.y - (float)iy;
+            const float sine = sincos_poly(ori, 0), cose = sincos_poly(ori, 1);
+            const float fracc = ((-sine) * fracy) + (cose * fracx);
+            const float fracr = (cose * fracy) + (sine * fracx);
+            const int iradius = f2i_rn((((1.4f * spacing) * (float)(wsz + 1)) * 0.5f) / (float)step);
+            const int side = 2 * iradius + 1;
+            const int nsamp = side * side;
+            const float fstep = (float)step;
+            for (int t = lane; t < nsamp; t += 64) {
+                const int si = t / side - iradius, sj = t % side - iradius;
+                const float fi = (float)si, fj = (float)sj;
+                const float rpos = ((fstep * ((cose * fi) + (sine * fj))) - fracr) / spacing;
+                const float cpos = ((fstep * (((-sine) * fi) + (cose * fj))) - fracc) / spacing;
+                const float rx = rpos + wofs, cx = cpos + wofs;
+                if (!(rx > -1.f && rx < fw && cx > -1.f && cx < fw)) continue;
+                const int r = iy + si * step, c = ix + sj * step;
+                if (!(r >= 1 + hs && r < rlim && c >= 1 + hs && c < clim)) continue;
+                const float weight = c_tab.lut2[f2i_rz(rpos * rpos + cpos * cpos)];
+                const float dxx = (weight * (float)wavelet2(I, ip, c, r, hs)) * INV255;
+                const float dyy = (weight * (float)wavelet1(I, ip, c, r, hs)) * INV255;
+                const float dx = (cose * dxx) + (sine * dyy);
+                const float dy = (sine * dxx) - (cose * dyy);
+                if (!P.extend) {
+                    place(d, wsz, osz, dx, (dx < 0 ? 0 : 1), dy, (dy < 0 ? 2 : 3), rx, cx);
+                } else {
+                    place(d, wsz, osz, dx, (dy < 0 ? 0 : 1), fabsf(dx), (dy < 0 ? 2 : 3), rx, cx);
+                    place(d, wsz, osz, dy, (dx < 0 ? 4 : 5), fabsf(dy), (dx < 0 ? 6 : 7), rx, cx);
+                }
+            }
+        }
+        wave_sync();
+        // normalize (surfd.cu:2447-2493): sequential-addressing tree
+        const float v0 = lane < (unsigned)nf ? d[lane] : 0.f;
+        const float v1 = (nf > 64 && lane + 64 < (unsigned)nf) ? d[lane + 64] : 0.f;
+        float a = v0 * v0;
+        if (nf > 64) a = a + v1 * v1;
+#pragma unroll
+        for (int k = 32; k >= 1; k >>= 1) a = a + __shfl_down(a, k, 64);
+        const float tot = __shfl(a, 0, 64);
+        const float fac = 1.f / sqrtf(tot);
+        float* out = desc + ((size_t)f * max_pts + i) * nf;
+        if (lane < (unsigned)nf) out[lane] = v0 * fac;
+        if (nf > 64 && lane + 64 < (unsigned)nf) out[lane + 64] = v1 * fac;
+        wave_sync();
+    }
+}
+
+hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
+                           const int* counts, const int* offsets, int nframes, float* desc, hipStream_t s)
+{
+    if (P.nfeat > 128) return hipErrorInvalidValue;
+    const int grid = 2048;
+    if (P.upright) k_describe<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, counts, offsets, nframes, desc);
+    else k_describe<false><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, counts, offsets, nframes, desc);
+    return hipGetLastError();
+}
+
+// ======================================================================
+// Result slab packing for the multi-GPU all-gather.
+// ======================================================================
+__global__ __launch_bounds__(256) void k_pack(const surfhip_point* __restrict__ pts, const float* __restrict__ desc,
+                                              const int* __restrict__ counts, int max_pts, int nfeat,
+                                              size_t slab_bytes, uint8_t* __restrict__ slab)
+{
+    const int f = blockIdx.y;
+    uint8_t* base = slab + (size_t)f * slab_bytes;
+    const int cnt = counts[f];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        reinterpret_cast<int*>(base)[0] = cnt;
+        reinterpret_cast<int*>(base)[1] = max_pts;
+        reinterpret_cast<int*>(base)[2] = nfeat;
+        reinterpret_cast<int*>(base)[3] = 0;
+    }
+    surfhip_point* pout = reinterpret_cast<surfhip_point*>(base + 16);
+    float* dout = reinterpret_cast<float*>(base + 16 + (size_t)max_pts * sizeof(surfhip_point));
+    const size_t tid = (size_t)blockIdx.x * 256 + threadIdx.x, stride = (size_t)gridDim.x * 256;
+    for (size_t t = tid; t < (size_t)cnt; t += stride) pout[t] = pts[(size_t)f * max_pts + t];
+    if (desc)
+        for (size_t t = tid; t < (size_t)cnt * nfeat; t += stride) dout[t] = desc[(size_t)f * max_pts * nfeat + t];
+}
+
+hipError_t launch_pack(const surfhip_point* pts, const float* desc, const int* counts, int nframes,
+                       int max_pts, int nfeat, size_t slab_bytes, uint8_t* slab, hipStream_t s)
+{
+    k_pack<<<dim3(64, nframes), 256, 0, s>>>(pts, desc, counts, max_pts, nfeat, slab_bytes, slab);
+    return hipGetLastError();
+}
+
+}  // namespace surfhip

@@ -1,0 +1,188 @@
+/*
+ * surfhip.h -- the C-ABI boundary of the MI355X SURF engine (libsurfhip.so).
+ *
+ * Plain C: plain pointers, sizes and int status codes; no HIP, torch or C++
+ * types.  Device pointers are `void*`/typed pointers into HBM allocated with
+ * surfhip_malloc (or by any HIP user in the same process, e.g. PyTorch).
+ *
+ * Every entry point names the reference interface it replaces (file:line in
+ * the CUDA-SURF reference).  The C++ drop-in layer (include/surf.h,
+ * include/cuda_utils.h, cuda-surf_amd/csrc/surf.cpp) is built only on these.
+ */
+#ifndef SURFHIP_H
+#define SURFHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (replaces cudaError_t in CHECK(), cuda_utils.h:18-25) */
+#define SURFHIP_OK               0
+#define SURFHIP_ERR_INVALID     -1   /* bad argument / shape              */
+#define SURFHIP_ERR_HIP         -2   /* HIP runtime error (see last error) */
+#define SURFHIP_ERR_CAPACITY    -3   /* candidate buffer overflowed        */
+#define SURFHIP_ERR_UNSUPPORTED -4   /* option outside the built path      */
+#define SURFHIP_ERR_NOMEM       -5
+
+/* copy kinds (cudaMemcpyKind) */
+#define SURFHIP_H2H 0
+#define SURFHIP_H2D 1
+#define SURFHIP_D2H 2
+#define SURFHIP_D2D 3
+
+#ifdef __cplusplus
+#define SURFHIP_BOOL bool
+#else
+#define SURFHIP_BOOL _Bool
+#endif
+
+/* Byte-identical to surf::SurfParam (surf_structures.h:45-72, 48 B). */
+typedef struct surfhip_param {
+    float thresh;
+    int   init_lobe;
+    SURFHIP_BOOL doubled;
+    int   max_scale;
+    int   noctaves;
+    int   sampling;
+    float divisor;
+    SURFHIP_BOOL upright;
+    SURFHIP_BOOL extend;
+    int   desc_wsz;
+    int   mag_factor;
+    int   orient_size;
+    int   nfeatures;
+} surfhip_param;
+
+/* Byte-identical to surf::SurfPoint (surf_structures.h:10-30, 48 B). */
+typedef struct surfhip_point {
+    float x, y, scale;
+    int   o;
+    float strength;
+    int   laplace;
+    float ori, score;
+    int   match;
+    float match_x, match_y, ambiguity;
+} surfhip_point;
+
+/* ------------------------------------------------------------ runtime --
+ * Replaces cuda_utils.h:41-108 (initDevice, GpuTimer) and the cudart calls
+ * main.cpp makes through it (main.cpp:16, 97, 100, 155, 219-226, 273-281). */
+const char* surfhip_error_string(int status);     /* cudaGetErrorString      */
+int  surfhip_last_hip_error(void);                /* raw hipError_t of the last failure */
+int  surfhip_get_device_count(int* count);        /* cudaGetDeviceCount      */
+int  surfhip_set_device(int dev);                 /* cudaSetDevice           */
+int  surfhip_get_device(int* dev);
+int  surfhip_device_name(int dev, char* buf, int len, int* cu_count);
+int  surfhip_versions(int* driver, int* runtime); /* cudaDriver/RuntimeGetVersion */
+int  surfhip_malloc(void** ptr, size_t bytes);    /* cudaMalloc              */
+int  surfhip_malloc_pitch(void** ptr, size_t* pitch, size_t width_bytes, size_t height); /* cudaMallocPitch */
+int  surfhip_free(void* ptr);                     /* cudaFree                */
+int  surfhip_memset(void* ptr, int value, size_t bytes);             /* cudaMemset */
+int  surfhip_memset_async(void* ptr, int value, size_t bytes, void* stream);
+int  surfhip_memcpy(void* dst, const void* src, size_t bytes, int kind);  /* cudaMemcpy */
+int  surfhip_memcpy_async(void* dst, const void* src, size_t bytes, int kind, void* stream);
+int  surfhip_memcpy2d(void* dst, size_t dpitch, const void* src, size_t spitch,
+                      size_t width_bytes, size_t height, int kind);     /* cudaMemcpy2D */
+int  surfhip_device_synchronize(void);            /* cudaDeviceSynchronize   */
+int  surfhip_device_reset(void);                  /* cudaDeviceReset         */
+int  surfhip_stream_create(void** stream);
+int  surfhip_stream_destroy(void* stream);
+int  surfhip_stream_synchronize(void* stream);
+int  surfhip_event_create(void** ev);             /* cudaEventCreate (GpuTimer) */
+int  surfhip_event_destroy(void* ev);
+int  surfhip_event_record(void* ev, void* stream);
+int  surfhip_event_synchronize(void* ev);
+int  surfhip_event_elapsed(float* ms, void* start, void* stop);
+
+/* ----------------------------------------------------------- detector --
+ * One detector = one geometry (W x H) + SurfParam + scratch for up to
+ * max_batch frames, bound to one HIP stream.  Replaces the process-global
+ * __constant__/__device__ state of surfd.cu:13-24 and the scratch members of
+ * Surfor (surf.h:43-53), so several detectors (one per GPU / host thread)
+ * can coexist. */
+typedef struct surfhip_detector surfhip_detector;
+
+/* Surfor::init + allocMemory (surf.cpp:60-91, 374-415).  `param` must come
+ * from surfhip_make_param.  cand_cap = per-frame candidate capacity before
+ * the canonical sort (0 = default 65536).  stream = hipStream_t or NULL. */
+int surfhip_detector_create(surfhip_detector** det, const surfhip_param* param,
+                            int width, int height, int max_batch, int max_pts,
+                            int cand_cap, void* stream);
+int surfhip_detector_destroy(surfhip_detector* det);
+int surfhip_detector_set_stream(surfhip_detector* det, void* stream);
+
+/* Surfor::init parameter derivation (surf.cpp:63-79); returns
+ * SURFHIP_ERR_UNSUPPORTED for doubled=true (out of scope). */
+int surfhip_make_param(surfhip_param* out, int noctaves, float thresh, int doubled,
+                       int init_mask_size, int sampling_step, int upright,
+                       int extend, int desc_wsz);
+
+/* Batched detect+describe, asynchronous on the detector's stream.
+ * Replaces the per-frame sequence cuIntegral (surfd.cu:2683) ->
+ * cuHalfImage/cuCalcHessianMulti/cuFindMaximumWithInterp per octave
+ * (surf.cpp:248-294, surfd.cu:2775, 2829, 3058) -> cuDescribe (surfd.cu:3251).
+ *   d_frames : nframes u8 frames, row pitch `pitch` bytes (>= W, multiple of
+ *              16), frame f at d_frames + f*frame_stride (16-B aligned)
+ *   d_points : [nframes][max_pts] SurfPoint slots (device)
+ *   d_desc   : [nframes][max_pts][nfeatures] f32 (device) or NULL (desc=false)
+ *   d_counts : [nframes] int (device): keypoints kept per frame
+ * Keypoints of a frame are in canonical order (octave, nms level, row, col);
+ * descriptors are L2-normalised (surfd.cu:2447-2493). */
+int surfhip_detect_batch(surfhip_detector* det, const uint8_t* d_frames, int nframes,
+                         int pitch, size_t frame_stride, surfhip_point* d_points,
+                         float* d_desc, int* d_counts);
+
+/* Surfor::detectAndCompute (surf.cpp:205-355) for one frame, synchronous.
+ * Writes min(found, max_pts) SurfPoints to d_points, returns the count in
+ * *num_pts; when desc != 0 allocates *d_desc_out = num_pts*nfeatures floats
+ * (caller frees with surfhip_free, as main.cpp:275-282 does with cudaFree). */
+int surfhip_detect(surfhip_detector* det, const uint8_t* d_image, int pitch,
+                   surfhip_point* d_points, int max_pts, int* num_pts,
+                   float** d_desc_out, int desc);
+
+/* Raw candidate count per frame of the last call (before the max_pts clamp,
+ * surf.cpp:302-303); host array of nframes ints. */
+int surfhip_detector_candidates(surfhip_detector* det, int* h_counts, int nframes);
+
+/* Stage timing (HIP events on the detector's stream) for the last
+ * detect_batch: ms[0..5] = integral, hessian, nms, sort, describe, total. */
+#define SURFHIP_NSTAGE 6
+int surfhip_detector_set_profiling(surfhip_detector* det, int on);
+int surfhip_detector_stage_times(surfhip_detector* det, float* ms);
+
+/* Workspace access for parity tests: device pointers to frame 0's integral
+ * image ((H+1) x ipitch int32, frame stride ii_stride ints) and response
+ * planes (resp_stride floats per frame; octave o plane s at
+ * ooff[o] + s*osize[o], row pitch swhp[o].z). */
+int surfhip_detector_workspace(surfhip_detector* det, int32_t** d_ii, size_t* ii_stride,
+                               float** d_resp, size_t* resp_stride);
+int surfhip_detector_geometry(surfhip_detector* det, int* iwhp /*3*/, int* swhp /*3*8*/,
+                              long long* ooff /*8*/, int* osize /*8*/);
+
+/* Stage-level entry points on frames already resident (parity tests and the
+ * Hessian roofline run): integral only, Hessian only (needs integral). */
+int surfhip_run_integral(surfhip_detector* det, const uint8_t* d_frames, int nframes,
+                         int pitch, size_t frame_stride);
+int surfhip_run_hessian(surfhip_detector* det, int nframes);
+
+/* Algorithmic (compulsory) HBM bytes per frame of the Hessian stage:
+ * integral image read once + valid responses written. */
+long long surfhip_hessian_bytes_per_frame(surfhip_detector* det);
+
+/* Result slab for the multi-GPU all-gather: per frame
+ * [count int32][pad to 16 B][max_pts SurfPoint][max_pts*nfeatures f32].
+ * Pack nframes frames' results into d_slab (device, slab_bytes*nframes). */
+size_t surfhip_slab_bytes(int max_pts, int nfeatures);
+int surfhip_pack_slab(surfhip_detector* det, const surfhip_point* d_points, const float* d_desc,
+                      const int* d_counts, int nframes, void* d_slab);
+
+/* Library build identification (for the loaded-.so audit). */
+const char* surfhip_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SURFHIP_H */

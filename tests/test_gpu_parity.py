@@ -1,0 +1,218 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle.
+
+Bar (BASELINE.json north_star): integral image and Hessian planes bit-exact;
+keypoint tuple (x, y, scale, octave, strength, laplace sign) bit-exact;
+orientation bit-exact (deterministic reduction order on both sides);
+descriptors within 1e-4 L2 per keypoint (float atomics order).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, REF_DATA, assert_points_equal, canonical, desc_l2
+
+pytestmark = pytest.mark.gpu
+
+DESC_TOL = 1e-4
+
+
+def gpu_run(surf, param, frames, w, h, max_pts=16384, desc=True, want_ws=False, cand_cap=0):
+    """Upload frames [n, H, pitch], run detect_batch, return per-frame results."""
+    n, _, pitch = frames.shape
+    stride = h * pitch
+    det = surf.Detector(param, w, h, max_batch=n, max_pts=max_pts, cand_cap=cand_cap)
+    fb = surf.DeviceBuffer(frames.nbytes)
+    fb.upload(frames)
+    nf = param.nfeatures
+    pb = surf.DeviceBuffer(48 * n * max_pts)
+    db = surf.DeviceBuffer(4 * n * max_pts * nf) if desc else None
+    cb = surf.DeviceBuffer(4 * n)
+    det.detect_batch(fb.ptr, n, pitch, stride, pb.ptr, db.ptr if desc else None, cb.ptr)
+    surf.synchronize()
+    counts = cb.download(np.int32, n)
+    pts = pb.download(surf.POINT_DTYPE, n * max_pts).reshape(n, max_pts)
+    ds = db.download(np.float32, n * max_pts * nf).reshape(n, max_pts, nf) if desc else None
+    out = {"counts": counts, "pts": [pts[f, :counts[f]] for f in range(n)],
+           "desc": [ds[f, :counts[f]] for f in range(n)] if desc else None,
+           "cand": det.candidates(n)}
+    if want_ws:
+        ii, iis, rs, rss = det.workspace()
+        out["ii"] = surf.download_ptr(ii, np.int32, n * iis).reshape(n, -1)
+        out["resp"] = surf.download_ptr(rs, np.float32, n * rss).reshape(n, -1)
+        out["geom"] = det.geometry()
+    det.close()
+    return out
+
+
+def compare_frame(g_pts, g_desc, o_pts, o_desc, upright):
+    assert_points_equal(g_pts, o_pts)
+    if not upright:
+        same = g_pts["ori"].view(np.uint32) == o_pts["ori"].view(np.uint32)
+        assert same.all(), f"ori differs at {int(np.argmin(same))}"
+    if g_desc is not None:
+        err = desc_l2(g_desc, o_desc)
+        assert err.max() <= DESC_TOL, f"descriptor L2 max {err.max():.3g} at {int(err.argmax())}"
+
+
+@pytest.mark.parametrize("w,h", [(64, 48), (321, 241), (640, 480), (1920, 1080)])
+def test_integral_bit_exact(surf, orc, w, h):
+    frames = surf.synth_frames(2, w, h)
+    param = surf.make_param(4, 4.0, upright=True)
+    det = surf.Detector(param, w, h, max_batch=2, max_pts=1024)
+    fb = surf.DeviceBuffer(frames.nbytes)
+    fb.upload(frames)
+    det.run_integral(fb.ptr, 2, frames.shape[2], h * frames.shape[2])
+    surf.synchronize()
+    ii, iis, _, _ = det.workspace()
+    got = surf.download_ptr(ii, np.int32, 2 * iis).reshape(2, h + 1, -1)
+    for f in range(2):
+        ref = orc.integral(frames[f], w, h)
+        np.testing.assert_array_equal(got[f][:, :w + 1], ref[:, :w + 1])
+    det.close()
+
+
+def test_integral_saturated_4k_wraparound(surf, orc):
+    """All-255 3840x2160: the int32 image tops out at 2,115,072,000 (< 2^31) and
+    getSum's pairwise adds wrap."""
+    w, h = 3840, 2160
+    frames = np.full((1, h, surf.align_up(w, 128)), 255, np.uint8)
+    param = surf.make_param(5, 4.0, upright=True)
+    det = surf.Detector(param, w, h, max_batch=1, max_pts=1024)
+    fb = surf.DeviceBuffer(frames.nbytes)
+    fb.upload(frames)
+    det.run_integral(fb.ptr, 1, frames.shape[2], 0)
+    surf.synchronize()
+    ii, iis, _, _ = det.workspace()
+    got = surf.download_ptr(ii, np.int32, iis).reshape(h + 1, -1)
+    assert got[h, w] == 255 * w * h
+    ref = orc.integral(frames[0], w, h)
+    np.testing.assert_array_equal(got[:, :w + 1], ref[:, :w + 1])
+    det.close()
+
+
+def _plane_views(resp, g, octs, p):
+    """Yield (octave, scale, plane[sh, sw]) for every plane the Hessian computes."""
+    for o in range(p.noctaves):
+        sw, sh, sp = g.swhp[o].x, g.swhp[o].y, g.swhp[o].z
+        for s in range(p.max_scale):
+            base = g.ooff[o] + s * g.osize[o]
+            yield o, s, resp[base:base + sh * sp].reshape(sh, sp)[:, :sw]
+
+
+@pytest.mark.parametrize("w,h", [(640, 480), (1920, 1080)])
+def test_hessian_planes_bit_exact(surf, orc, w, h):
+    frames = surf.synth_frames(1, w, h, first=7)
+    param = surf.make_param(4, 4.0, upright=True)
+    res = gpu_run(surf, param, frames, w, h, want_ws=True, desc=False)
+    op = orc.make_param(4, 4.0, upright=True)
+    _, ref, g, octs = orc.hessian(op, frames[0], w, h)
+    got = res["resp"][0]
+    for (o, s, rp), (_, _, gp) in zip(_plane_views(ref, g, octs, op), _plane_views(got, g, octs, op)):
+        same = rp.view(np.uint32) == gp.view(np.uint32)
+        assert same.all(), f"octave {o} scale {s}: {(~same).sum()} cells differ, first at {np.argwhere(~same)[0]}"
+
+
+@pytest.mark.parametrize("upright,extend", [(True, False), (False, False), (True, True), (False, True)])
+def test_detect_describe_synthetic(surf, orc, upright, extend):
+    w, h = 640, 480
+    frames = surf.synth_frames(3, w, h, first=100)
+    param = surf.make_param(4, 4.0, upright=upright, extend=extend)
+    res = gpu_run(surf, param, frames, w, h)
+    op = orc.make_param(4, 4.0, upright=upright, extend=extend)
+    for f in range(3):
+        o_pts, o_desc, nc = orc.detect(op, frames[f], w, h)
+        assert res["cand"][f] == nc
+        compare_frame(res["pts"][f], res["desc"][f], o_pts, o_desc, upright)
+
+
+def test_detect_describe_1080p(surf, orc):
+    """Config #2: single 1920x1080, 4 octaves, 64-D, upright (main.cpp:187-204)."""
+    w, h = 1920, 1080
+    frames = surf.synth_frames(1, w, h)
+    param = surf.make_param(4, 4.0, upright=True)
+    res = gpu_run(surf, param, frames, w, h)
+    op = orc.make_param(4, 4.0, upright=True)
+    o_pts, o_desc, _ = orc.detect(op, frames[0], w, h)
+    assert len(o_pts) > 1000
+    assert set(np.unique(o_pts["o"])) == {0, 1, 2, 3}
+    compare_frame(res["pts"][0], res["desc"][0], o_pts, o_desc, True)
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(GOLDEN, "left_1280x960_upright.npz")),
+                    reason="golden fixtures not generated")
+@pytest.mark.parametrize("name", ["left_1280x960_upright", "left_1280x960_rotated", "right_1280x960_upright",
+                                  "left_640x480_upright", "left_1280x960_rotated_ext"])
+def test_golden_fixtures(surf, name):
+    """data/left.pgm / right.pgm (the reference's only data) vs frozen oracle outputs."""
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    img = z["image"]
+    h, w = img.shape
+    meta = z["meta"]
+    upright, extend = bool(meta[0]), bool(meta[1])
+    pitch = surf.align_up(w, 128)
+    frames = np.zeros((1, h, pitch), np.uint8)
+    frames[0, :, :w] = img
+    param = surf.make_param(4, 4.0, upright=upright, extend=extend)
+    res = gpu_run(surf, param, frames, w, h)
+    pts = np.frombuffer(z["points"].tobytes(), dtype=surf.POINT_DTYPE)
+    compare_frame(res["pts"][0], res["desc"][0], pts, z["desc"], upright)
+
+
+def test_batch_equals_single(surf):
+    """Frames processed in one batch give the same results as one at a time."""
+    w, h = 320, 240
+    frames = surf.synth_frames(4, w, h, first=55)
+    param = surf.make_param(4, 4.0, upright=False)
+    batch = gpu_run(surf, param, frames, w, h)
+    for f in range(4):
+        one = gpu_run(surf, param, frames[f:f + 1], w, h)
+        assert_points_equal(one["pts"][0], batch["pts"][f], fields=("x", "y", "scale", "o", "strength", "laplace", "ori"))
+        assert desc_l2(one["desc"][0], batch["desc"][f]).max() <= DESC_TOL
+
+
+def test_max_pts_cap_keeps_canonical_prefix(surf, orc):
+    w, h = 640, 480
+    frames = surf.synth_frames(1, w, h, first=3)
+    param = surf.make_param(4, 4.0, upright=True)
+    full = gpu_run(surf, param, frames, w, h, max_pts=16384)
+    cap = max(1, len(full["pts"][0]) // 3)
+    part = gpu_run(surf, param, frames, w, h, max_pts=cap)
+    assert part["counts"][0] == cap
+    assert_points_equal(part["pts"][0], full["pts"][0][:cap])
+    op = orc.make_param(4, 4.0, upright=True)
+    o_pts, _, _ = orc.detect(op, frames[0], w, h, max_pts=cap, desc=False)
+    assert_points_equal(part["pts"][0], o_pts)
+
+
+def test_flat_and_tiny_frames(surf):
+    """Edge cases: a constant frame yields no keypoints; a tiny frame works."""
+    param = surf.make_param(4, 4.0, upright=True)
+    flat = np.full((2, 96, 128), 77, np.uint8)
+    r = gpu_run(surf, param, flat, 100, 96)
+    assert (r["counts"] == 0).all()
+    tiny = surf.synth_frames(1, 40, 36)
+    r = gpu_run(surf, param, tiny, 40, 36)
+    assert r["counts"][0] >= 0
+
+
+def test_surfor_mirror_api(surf, orc):
+    """The reference-shaped API (Surfor.init / detectAndCompute, surf.h)."""
+    w, h = 640, 480
+    frame = surf.synth_frames(1, w, h, first=11)[0]
+    d = surf.Surfor()
+    d.init(4, 4.0, False, 9, 2, True, False, 4, w, h)
+    data = surf.initSurfData(10000, True, True)
+    img = surf.DeviceBuffer(frame.nbytes)
+    img.upload(frame)
+    dptr = d.detectAndCompute(img.ptr, data, (w, h, frame.shape[1]), True)
+    op = orc.make_param(4, 4.0, upright=True)
+    o_pts, o_desc, _ = orc.detect(op, frame, w, h)
+    assert data.num_pts == len(o_pts)
+    assert_points_equal(data.h_data[:data.num_pts], o_pts)
+    got = surf.download_ptr(dptr, np.float32, data.num_pts * 64).reshape(-1, 64)
+    assert desc_l2(got, o_desc).max() <= DESC_TOL
+    surf.check(surf.lib.surfhip_free(dptr))
+    surf.freeSurfData(data)
