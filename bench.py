@@ -1,0 +1,264 @@
+#!/usr/bin/env python3
+"""bench.py -- SURF detect+describe throughput on MI355X.
+
+Metric (BASELINE.json): 1080p frames/sec (detect+describe); keypoints/s is
+reported beside it.  Workload (config #3, the HBM-bound Hessian roofline run):
+a batch of 256 synthetic 1920x1080 u8 frames per GPU, 4 octaves, 64-D upright
+descriptors, thresh=4, sampling 2, init mask 9 (main.cpp:187-204), resident
+in HBM before the timed region.  One step = the whole hot path over one batch:
+integral -> Hessian (all octaves) -> NMS + interpolation -> canonical sort ->
+descriptors.  With N > 1 GPUs (one process per GPU, torch.distributed over
+RCCL) each rank processes its own 256 frames (weak scaling, config #4 at
+N = 8) and the compacted SurfPoint + descriptor slab of every rank is
+all-gathered over xGMI; the gather of batch i overlaps the
+compute of batch i+1.
+
+Rank 0 prints ONE JSON line (the driver's contract), with a `roofline` object
+for the Hessian kernel (HIP events on the detector's stream inside the timed
+region; algorithmic bytes = integral image read once + valid responses
+written) and a `cpu_baseline` object (the oracle/ CPU restatement on a
+bounded sample of the same frames, rank 0 at N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import importlib.util
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def load_surf():
+    pkg = os.path.join(REPO, "cuda-surf_amd")
+    spec = importlib.util.spec_from_file_location("surf_amd", os.path.join(pkg, "__init__.py"),
+                                                  submodule_search_locations=[pkg])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["surf_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def cpu_baseline(frames, w, h, args):
+    """The oracle (a scalar C restatement of the reference) on a bounded sample."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # test infrastructure: the baseline only, never the measured path
+    n = min(args.cpu_frames, frames.shape[0])
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    p = oracle.make_param(args.octaves, args.thresh, False, 9, 2, bool(args.upright), bool(args.extend), 4)
+    secs, pts = oracle.bench_frames(p, frames[:n], w, h, args.max_pts, threads)
+    return {"value": round(n / secs, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{n} of the {frames.shape[0]} synthetic {w}x{h} frames, detect+describe, "
+                      f"one frame per thread, {threads} threads, {pts} keypoints, {secs:.2f} s wall"}
+
+
+def pmc_traffic(args):
+    """Per-launch HBM bytes of the Hessian kernel from a committed rocprofv3
+    --pmc summary (profiles/*hessian_pmc.json), or None."""
+    path = args.pmc_json or os.path.join(REPO, "profiles", "hessian_pmc.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        if d.get("config") == f"{args.batch}x{args.width}x{args.height}x{args.octaves}":
+            return float(d["bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="frames per GPU per step")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--octaves", type=int, default=4)
+    ap.add_argument("--upright", type=int, default=1)
+    ap.add_argument("--extend", type=int, default=0)
+    ap.add_argument("--thresh", type=float, default=4.0)
+    ap.add_argument("--max-pts", type=int, default=16384)
+    ap.add_argument("--cpu-frames", type=int, default=128)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="no HIP events in the timed region")
+    ap.add_argument("--pmc-json", default=None)
+    ap.add_argument("--hessian-only", action="store_true",
+                    help="time only the Hessian stage (for rocprofv3 --pmc passes)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # torch first: its HIP runtime is the one copy in this process
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+    surf = load_surf()
+    surf.set_device(dev.index)
+
+    W, H, B = args.width, args.height, args.batch
+    pitch = surf.align_up(W, 128)
+    t0 = time.time()
+    first, _ = surf.dist.shard_range(world * B, world, rank)   # rank r: frames [r*B, (r+1)*B)
+    frames = surf.synth_frames(B, W, H, pitch, first=first)
+    gen_s = time.time() - t0
+    d_frames = torch.from_numpy(frames).to(dev)
+    param = surf.make_param(args.octaves, args.thresh, False, 9, 2, bool(args.upright), bool(args.extend), 4)
+    nf = param.nfeatures
+    stream = torch.cuda.current_stream(dev)
+    det = surf.Detector(param, W, H, max_batch=B, max_pts=args.max_pts, stream=stream.cuda_stream)
+    d_pts = torch.empty(B * args.max_pts * 48, dtype=torch.uint8, device=dev)
+    d_desc = torch.empty(B * args.max_pts * nf, dtype=torch.float32, device=dev)
+    d_cnt = torch.zeros(B, dtype=torch.int32, device=dev)
+    profile = not args.no_profile
+    det.set_profiling(profile)
+
+    def run_batch():
+        if args.hessian_only:
+            det.run_hessian(B)
+        else:
+            det.detect_batch(d_frames.data_ptr(), B, pitch, H * pitch, d_pts.data_ptr(), d_desc.data_ptr(),
+                             d_cnt.data_ptr())
+
+    if args.hessian_only:
+        det.run_integral(d_frames.data_ptr(), B, pitch, H * pitch)
+
+    # multi-GPU exchange: compacted slabs, double-buffered, gather(i-1) || compute(i)
+    slabs = [None, None]
+    gathered = [None, None]
+    pending = None
+
+    def launch_gather(i):
+        total = det.batch_total(B)                    # sync: sizes the collective
+        cap = surf.dist.agree_slab_size(dist, torch, det.slab_bytes(B, total), dev)
+        k = i & 1
+        if slabs[k] is None or slabs[k].numel() < cap:
+            slabs[k] = torch.empty(int(cap * 1.25) + 4096, dtype=torch.uint8, device=dev)
+            gathered[k] = torch.empty(world * slabs[k].numel(), dtype=torch.uint8, device=dev)
+        det.pack_slab(d_pts.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(), B, slabs[k].data_ptr())
+        _, work = surf.dist.allgather_slabs(dist, torch, slabs[k], cap, world, out=gathered[k], async_op=True)
+        return work
+
+    def step(i):
+        nonlocal pending
+        run_batch()
+        if world > 1 and not args.hessian_only:
+            if pending is not None:
+                pending.wait()
+            pending = launch_gather(i)
+
+    for i in range(args.warmup):
+        step(i)
+    if pending is not None:
+        pending.wait()
+        pending = None
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    stage_acc = {}
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+        if profile and not args.hessian_only:
+            for k, v in det.stage_times().items():
+                stage_acc[k] = stage_acc.get(k, 0.0) + v
+    if pending is not None:
+        pending.wait()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    counts = d_cnt.cpu().numpy()
+    kp_per_batch = int(counts.sum())
+    if world > 1:
+        kt = torch.tensor([kp_per_batch], dtype=torch.int64, device=dev)
+        dist.all_reduce(kt)
+        kp_total_batch = int(kt.item())
+    else:
+        kp_total_batch = kp_per_batch
+
+    # Hessian stage alone (events on the detector's stream) when the timed
+    # loop did not record stage times
+    if args.hessian_only or not profile:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        if not args.hessian_only:
+            det.run_integral(d_frames.data_ptr(), B, pitch, H * pitch)
+        ev0.record(stream)
+        for _ in range(args.steps):
+            det.run_hessian(B)
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        hess_ms = ev0.elapsed_time(ev1) / args.steps
+    else:
+        hess_ms = stage_acc["hessian"] / args.steps
+
+    frames_total = world * B * args.steps
+    value = frames_total / elapsed
+    result = None
+    if rank == 0:
+        hb = det.hessian_bytes_per_frame() * B
+        achieved = hb / (hess_ms * 1e-3) / 1e9
+        traffic = pmc_traffic(args)
+        result = {
+            "metric": "1080p frames/sec (detect+describe)" if (W, H) == (1920, 1080) else f"{W}x{H} frames/sec (detect+describe)",
+            "value": round(value, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8/i32/f32",
+            "data": "synthetic (seeded Gaussian-blob 1080p frames, resident in HBM)",
+            "config": {"workload": f"config#3 batch {B} x {W}x{H} per GPU, {args.octaves} octaves, "
+                                   f"{nf}-D {'upright' if args.upright else 'rotated'} descriptors, thresh {args.thresh}"
+                                   + (", RCCL all-gather of compacted SurfPoint+descriptor slabs" if world > 1 else ""),
+                       "frames_per_gpu_per_step": B, "width": W, "height": H, "octaves": args.octaves,
+                       "nfeatures": nf, "upright": bool(args.upright), "parallelism": f"frames sharded x{world}"},
+            "keypoints_per_s": round(kp_total_batch * args.steps / elapsed, 1),
+            "keypoints_per_frame": round(kp_total_batch / (world * B), 1),
+            "stage_ms_per_step": {k: round(v / args.steps, 4) for k, v in stage_acc.items()},
+            "roofline": {"kernel": "k_hessian (all octaves, one launch per batch)", "bound": "hbm",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "algorithmic_bytes_per_launch": hb, "launch_ms": round(hess_ms, 4)},
+            "gen_s": round(gen_s, 2),
+        }
+        if world == 1 and not args.no_cpu and not args.hessian_only:
+            result["cpu_baseline"] = cpu_baseline(frames, W, H, args)
+        else:
+            result["cpu_baseline"] = None
+        print(json.dumps(result), flush=True)
+    det.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

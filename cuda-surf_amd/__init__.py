@@ -111,7 +111,8 @@ _sigs = {
     "surfhip_run_integral": (_i, [_vp, _vp, _i, _i, _sz]),
     "surfhip_run_hessian": (_i, [_vp, _i]),
     "surfhip_hessian_bytes_per_frame": (C.c_longlong, [_vp]),
-    "surfhip_slab_bytes": (_sz, [_i, _i]),
+    "surfhip_slab_bytes": (_sz, [_i, _i, _i]),
+    "surfhip_batch_total": (_i, [_vp, _i, C.POINTER(_i)]),
     "surfhip_pack_slab": (_i, [_vp, _vp, _vp, _vp, _i, _vp]),
     "surfhip_build_info": (C.c_char_p, []),
 }
@@ -294,8 +295,13 @@ class Detector:
     def hessian_bytes_per_frame(self) -> int:
         return int(_lib.surfhip_hessian_bytes_per_frame(self.h))
 
-    def slab_bytes(self) -> int:
-        return int(_lib.surfhip_slab_bytes(self.max_pts, self.nfeatures))
+    def slab_bytes(self, nframes: int, total: int, desc: bool = True) -> int:
+        return int(_lib.surfhip_slab_bytes(nframes, total, self.nfeatures if desc else 0))
+
+    def batch_total(self, nframes: int) -> int:
+        t = C.c_int()
+        check(_lib.surfhip_batch_total(self.h, nframes, C.byref(t)), "batch_total")
+        return t.value
 
     def pack_slab(self, points_ptr, desc_ptr, counts_ptr, nframes, slab_ptr) -> None:
         check(_lib.surfhip_pack_slab(self.h, points_ptr, desc_ptr, counts_ptr, nframes, slab_ptr), "pack_slab")
@@ -417,3 +423,35 @@ def downsample2(img: np.ndarray, w: int, h: int) -> np.ndarray:
     out = np.zeros((h // 2, pitch), np.uint8)
     _syn.surf_downsample2(src.ctypes.data, w, h, src.shape[1], out.ctypes.data, pitch)
     return out
+
+
+def parse_slab(buf: np.ndarray):
+    """Host view of one compacted result slab (see include/surfhip.h):
+    returns (counts[nframes], points[total], desc[total, nf] or None)."""
+    b = np.ascontiguousarray(buf).view(np.uint8)
+    nframes, total, nf, _ = (int(v) for v in b[:16].view(np.int32))
+    counts = b[16:16 + 4 * nframes].view(np.int32).copy()
+    head = 16 + ((4 * nframes + 15) & ~15)
+    pts = b[head:head + 48 * total].view(POINT_DTYPE).copy()
+    desc = None
+    if nf:
+        o = head + 48 * total
+        desc = b[o:o + 4 * total * nf].view(np.float32).reshape(total, nf).copy()
+    return counts, pts, desc
+
+
+def build_slab(counts: np.ndarray, pts: np.ndarray, desc) -> np.ndarray:
+    """Host-side builder of the same format (used by the CPU tests)."""
+    nframes, total = len(counts), int(counts.sum())
+    nf = 0 if desc is None else desc.shape[1]
+    head = 16 + ((4 * nframes + 15) & ~15)
+    out = np.zeros(head + total * (48 + 4 * nf), np.uint8)
+    out[:16].view(np.int32)[:] = (nframes, total, nf, 0)
+    out[16:16 + 4 * nframes].view(np.int32)[:] = counts
+    out[head:head + 48 * total] = np.ascontiguousarray(pts[:total]).view(np.uint8)
+    if nf:
+        out[head + 48 * total:] = np.ascontiguousarray(desc[:total], dtype=np.float32).view(np.uint8).ravel()
+    return out
+
+
+from . import dist  # noqa: E402  (multi-GPU sharding + slab all-gather helpers)

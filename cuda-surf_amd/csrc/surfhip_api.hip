@@ -48,6 +48,8 @@ struct surfhip_detector {
     surfhip_param param{};
     FrameParams P{};
     OctaveParams oct[kMaxOct]{};
+    OctaveParams* d_oct = nullptr;      // device copy read by the fused launches
+    LaunchPlan plan{};
     int W = 0, H = 0, max_batch = 0, max_pts = 0, cap = 0;
     int nbands = 0, CW = 0;
     size_t tot_osize = 0;
@@ -365,7 +367,7 @@ static int derive(surfhip_detector* d)
 
 static void free_all(surfhip_detector* d)
 {
-    void* ptrs[] = {d->ii, d->resp, d->colsum, d->cand, d->keys, d->gscratch, d->cand_count,
+    void* ptrs[] = {d->d_oct, d->ii, d->resp, d->colsum, d->cand, d->keys, d->gscratch, d->cand_count,
                     d->offsets, d->status, d->pts1, d->desc1, d->count1};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -408,6 +410,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
         e = hipMalloc((void**)&(ptr), (bytes));              \
         if (e != hipSuccess) goto fail;                      \
     } while (0)
+    ALLOC(d->d_oct, sizeof(OctaveParams) * kMaxOct);
     ALLOC(d->ii, B * d->P.ii_stride * sizeof(int32_t));
     ALLOC(d->resp, B * d->tot_osize * sizeof(float));
     ALLOC(d->colsum, B * d->nbands * d->CW * sizeof(uint32_t));
@@ -423,7 +426,9 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
 #undef ALLOC
     // zero once: integral pad columns and response pad columns are never
     // written by the kernels and never read by them either
-    e = hipMemset(d->ii, 0, B * d->P.ii_stride * sizeof(int32_t));
+    make_plan(d->P, d->oct, d->plan);
+    e = hipMemcpy(d->d_oct, d->oct, sizeof(OctaveParams) * kMaxOct, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(d->ii, 0, B * d->P.ii_stride * sizeof(int32_t));
     if (e == hipSuccess) e = hipMemset(d->resp, 0, B * d->tot_osize * sizeof(float));
     if (e == hipSuccess) e = hipMemset(d->status, 0, 16);
     if (e != hipSuccess) goto fail;
@@ -487,8 +492,7 @@ int surfhip_run_integral(surfhip_detector* d, const uint8_t* frames, int nframes
 int surfhip_run_hessian(surfhip_detector* d, int nframes)
 {
     if (!d || nframes < 1 || nframes > d->max_batch) return SURFHIP_ERR_INVALID;
-    for (int o = 0; o < d->param.noctaves; o++)
-        HIPCHK(launch_hessian(d->ii, d->resp, nframes, d->P, d->oct[o], o, d->stream));
+    HIPCHK(launch_hessian(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->stream));
     return SURFHIP_OK;
 }
 
@@ -504,12 +508,10 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
     if (prof) HIPCHK(hipEventRecord(d->ev[0], s));
     HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[1], s));
-    for (int o = 0; o < d->param.noctaves; o++)
-        HIPCHK(launch_hessian(d->ii, d->resp, nframes, d->P, d->oct[o], o, s));
+    HIPCHK(launch_hessian(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[2], s));
-    for (int o = 0; o < d->param.noctaves; o++)
-        HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->oct[o], o, d->cand, d->keys, d->cand_count,
-                          d->cap, s));
+    HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->cand, d->keys, d->cand_count,
+                      d->cap, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[3], s));
     HIPCHK(launch_sort(d->cand, d->keys, d->gscratch, d->cand_count, d->cap, nframes, points, d->max_pts,
                        counts, d->offsets, d->status, s));
@@ -602,18 +604,26 @@ int surfhip_detector_geometry(surfhip_detector* d, int* iwhp, int* swhp, long lo
 
 long long surfhip_hessian_bytes_per_frame(surfhip_detector* d) { return d ? d->hess_bytes : -1; }
 
-size_t surfhip_slab_bytes(int max_pts, int nfeatures)
+size_t surfhip_slab_bytes(int nframes, int total, int nfeatures)
 {
-    const size_t b = 16 + (size_t)max_pts * sizeof(surfhip_point) + (size_t)max_pts * nfeatures * sizeof(float);
-    return (b + 255) & ~(size_t)255;
+    return 16 + (((size_t)nframes * 4 + 15) & ~(size_t)15) +
+           (size_t)total * (sizeof(surfhip_point) + sizeof(float) * (size_t)nfeatures);
+}
+
+int surfhip_batch_total(surfhip_detector* d, int nframes, int* total)
+{
+    if (!d || !total || nframes < 1 || nframes > d->max_batch) return SURFHIP_ERR_INVALID;
+    HIPCHK(hipMemcpyAsync(total, d->offsets + nframes, sizeof(int), hipMemcpyDeviceToHost, d->stream));
+    HIPCHK(hipStreamSynchronize(d->stream));
+    return SURFHIP_OK;
 }
 
 int surfhip_pack_slab(surfhip_detector* d, const surfhip_point* pts, const float* desc, const int* counts,
                       int nframes, void* slab)
 {
-    if (!d || !pts || !counts || !slab || nframes < 1) return SURFHIP_ERR_INVALID;
-    const size_t sb = surfhip_slab_bytes(d->max_pts, d->param.nfeatures);
-    HIPCHK(launch_pack(pts, desc, counts, nframes, d->max_pts, d->param.nfeatures, sb, (uint8_t*)slab, d->stream));
+    if (!d || !pts || !counts || !slab || nframes < 1 || nframes > d->max_batch) return SURFHIP_ERR_INVALID;
+    HIPCHK(launch_pack(pts, desc, counts, d->offsets, nframes, d->max_pts, d->param.nfeatures, (uint8_t*)slab,
+                       d->stream));
     return SURFHIP_OK;
 }
 

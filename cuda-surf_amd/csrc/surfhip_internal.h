@@ -57,18 +57,27 @@ hipError_t set_tables(const Tables& t);
 
 hipError_t launch_integral(const uint8_t* frames, int pitch, long long fstride, int nframes,
                            const FrameParams& P, uint32_t* colsum, int32_t* ii, hipStream_t s);
+// Block ranges of the fused all-octave launches (computed once per detector).
+struct LaunchPlan {
+    int hess_start[kMaxOct + 1];    // Hessian blocks of octave o: [start[o], start[o+1])
+    int hess_nbx[kMaxOct];          // blocks per row of samples
+    int nms_start[kMaxOct + 1];     // NMS blocks of octave o (both levels)
+    int nms_nbx[kMaxOct], nms_nby[kMaxOct];
+};
+void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan);
+
 hipError_t launch_hessian(const int32_t* ii, float* resp, int nframes, const FrameParams& P,
-                          const OctaveParams& q, int o, hipStream_t s);
+                          const OctaveParams* d_oct, const LaunchPlan& plan, hipStream_t s);
 hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,
-                      const OctaveParams& q, int o, surfhip_point* cand, uint32_t* keys,
-                      int* cand_count, int cap, hipStream_t s);
+                      const OctaveParams* d_oct, const LaunchPlan& plan, surfhip_point* cand,
+                      uint32_t* keys, int* cand_count, int cap, hipStream_t s);
 hipError_t launch_sort(const surfhip_point* cand, const uint32_t* keys, uint64_t* gscratch,
                        int* cand_count, int cap, int nframes, surfhip_point* out, int max_pts,
                        int* out_count, int* offsets, int* status, hipStream_t s);
 hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
                            const int* counts, const int* offsets, int nframes, float* desc,
                            hipStream_t s);
-hipError_t launch_pack(const surfhip_point* pts, const float* desc, const int* counts, int nframes,
-                       int max_pts, int nfeat, size_t slab_bytes, uint8_t* slab, hipStream_t s);
+hipError_t launch_pack(const surfhip_point* pts, const float* desc, const int* counts, const int* offsets,
+                       int nframes, int max_pts, int nfeat, uint8_t* slab, hipStream_t s);
 
 }  // namespace surfhip

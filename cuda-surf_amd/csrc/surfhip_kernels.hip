@@ -2,7 +2,7 @@
 //
 // Stage map (reference file:line -> kernel here):
 //   integralRow/integralCol   surfd.cu:129-165, 2683-2704  -> k_ii_bandsum, k_ii_bandscan, k_ii_fill
-//   halfImage                 surfd.cu:321-331             -> folded into k_hessian (octaves > 0)
+//   halfImage                 surfd.cu:321-331             -> virtual planes read by k_nms (OctView)
 //   calcHessianMultiConst     surfd.cu:445-481, 2829-2894  -> k_hessian
 //   findMaximumWithInterp     surfd.cu:676-832, 3058-3079  -> k_nms
 //   (atomicInc emission order) surfd.cu:825-830            -> k_sort (canonical order + max_pts cap)
@@ -179,10 +179,15 @@ __global__ __launch_bounds__(256) void k_ii_fill(const uint8_t* __restrict__ fra
 #pragma unroll
         for (int k = 0; k < CPT; k++) acc[k] += px[k];
         if (active) {
+            // pad columns (> W) stay zero: the flat reads of getTrace can
+            // land on them (see trace_sign)
+            uint32_t o[CPT];
+#pragma unroll
+            for (int k = 0; k < CPT; k++) o[k] = (x0 + k <= W) ? acc[k] : 0u;
             uint32_t* dst = out + (size_t)(y0 + r + 1) * ip + x0;
 #pragma unroll
             for (int k = 0; k < CPT; k += 4)
-                *reinterpret_cast<uint4*>(dst + k) = make_uint4(acc[k], acc[k + 1], acc[k + 2], acc[k + 3]);
+                *reinterpret_cast<uint4*>(dst + k) = make_uint4(o[k], o[k + 1], o[k + 2], o[k + 3]);
         }
     }
 }
@@ -213,9 +218,9 @@ hipError_t launch_integral(const uint8_t* frames, int pitch, long long fstride, 
 // Hessian determinant (calcHessianMultiConst, surfd.cu:445-481; getHessian
 // surfd.cu:353-366).  One thread per response sample of one octave, all
 // scales of the octave; cells outside a scale's valid window are written 0
-// (the reference's cudaMemset, surf.cpp:348).  For octaves > 0 the same
-// thread also writes planes 0/1 from the previous octave's planes 2/4
-// (halfImage, surfd.cu:321-331).
+// (the reference's cudaMemset, surf.cpp:348).  Planes 0/1 of octaves > 0
+// (the reference's halfImage copies, surfd.cu:321-331) are never
+// materialised: k_nms reads them from the previous octave's planes 2/4.
 // ======================================================================
 
 // getSum (surfd.cu:334-343): inclusive rect [x2..x1] x [y2..y1].
@@ -247,40 +252,68 @@ __device__ __forceinline__ float hessian_at(const uint32_t* __restrict__ I, int 
     return rr * (a - b);
 }
 
-template <int NS>
-__global__ __launch_bounds__(256) void k_hessian(const int32_t* __restrict__ ii, float* __restrict__ resp,
-                                                 FrameParams P, OctaveParams q, int with_half)
+void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan)
 {
-    const int ix = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int iy = blockIdx.y * 4 + (threadIdx.x >> 6);
-    const int f = blockIdx.z;
+    int hb = 0, nb = 0;
+    for (int o = 0; o < kMaxOct; o++) {
+        plan.hess_start[o] = hb;
+        plan.nms_start[o] = nb;
+        if (o < P.noct) {
+            const OctaveParams& q = oct[o];
+            plan.hess_nbx[o] = (q.sw + 63) / 64;
+            hb += plan.hess_nbx[o] * ((q.sh + 3) / 4);
+            plan.nms_nbx[o] = (q.nms_gx + 63) / 64;
+            plan.nms_nby[o] = (q.nms_gy + 3) / 4;
+            nb += 2 * plan.nms_nbx[o] * plan.nms_nby[o];
+        } else {
+            plan.hess_nbx[o] = plan.nms_nbx[o] = plan.nms_nby[o] = 1;
+        }
+    }
+    plan.hess_start[kMaxOct] = hb;
+    plan.nms_start[kMaxOct] = nb;
+}
+
+__device__ __forceinline__ int octave_of(const int* start, int noct, int b)
+{
+    int o = 0;
+    while (o + 1 < noct && b >= start[o + 1]) o++;
+    return o;
+}
+
+// All octaves of a frame in one launch: blockIdx.x walks the octaves' sample
+// grids (64 x 4 samples per block), blockIdx.y is the frame.
+__global__ __launch_bounds__(256) void k_hessian(const int32_t* __restrict__ ii, float* __restrict__ resp,
+                                                 FrameParams P, const OctaveParams* __restrict__ oct,
+                                                 LaunchPlan plan)
+{
+    const int o = octave_of(plan.hess_start, P.noct, blockIdx.x);
+    const OctaveParams& q = oct[o];
+    const int lb = blockIdx.x - plan.hess_start[o];
+    const int nbx = plan.hess_nbx[o];
+    const int ix = (lb % nbx) * 64 + (threadIdx.x & 63);
+    const int iy = (lb / nbx) * 4 + (threadIdx.x >> 6);
+    const int f = blockIdx.y;
     if (ix >= q.sw || iy >= q.sh) return;
     const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
-    float* F = resp + (size_t)f * P.resp_stride;
-    float* R = F + q.ooff + (size_t)iy * q.sp + ix;
+    float* R = resp + (size_t)f * P.resp_stride + q.ooff + (size_t)iy * q.sp + ix;
     const int x0 = q.delta * ix, y0 = q.delta * iy;
+    const int ns = q.nscale;
 #pragma unroll
-    for (int i = 0; i < NS; i++) {
+    for (int i = 0; i < kMaxScale; i++) {
+        if (i >= ns) break;
         const int b1 = q.b1[i];
         float v = 0.f;
         if (ix >= b1 && ix < q.sw - b1 && iy >= b1 && iy < q.sh - b1)
             v = hessian_at(I, P.ip, x0, y0, q.mask[i], q.x2[i], q.x3[i], q.x4[i]) * q.norm[i];
         R[(size_t)(q.init_scale + i) * q.osize] = v;
     }
-    if (with_half) {
-        const float* src = F + q.pooff + (size_t)(2 * iy) * q.psp + 2 * ix;
-        R[0] = src[(size_t)2 * q.posize];
-        R[(size_t)q.osize] = src[(size_t)4 * q.posize];
-    }
 }
 
 hipError_t launch_hessian(const int32_t* ii, float* resp, int nframes, const FrameParams& P,
-                          const OctaveParams& q, int o, hipStream_t s)
+                          const OctaveParams* d_oct, const LaunchPlan& plan, hipStream_t s)
 {
-    dim3 grid((q.sw + 63) / 64, (q.sh + 3) / 4, nframes);
-    if (q.nscale == 5) k_hessian<5><<<grid, 256, 0, s>>>(ii, resp, P, q, o > 0);
-    else if (q.nscale == 3) k_hessian<3><<<grid, 256, 0, s>>>(ii, resp, P, q, o > 0);
-    else return hipErrorInvalidValue;
+    dim3 grid(plan.hess_start[kMaxOct], nframes);
+    k_hessian<<<grid, 256, 0, s>>>(ii, resp, P, d_oct, plan);
     return hipGetLastError();
 }
 
@@ -321,24 +354,37 @@ __device__ void solve3(float* sol, float (&sq)[3][3])
     }
 }
 
-__device__ float fit_quad(const float* __restrict__ src, float (&off)[3], int s, int r, int c, int osize, int sp)
+// Response planes of one octave as the reference lays them out after its
+// halfImage copies: planes 0/1 of octave o > 0 are read in place from octave
+// o-1's planes 2/4 at (2r, 2c), which is exactly what halfImage copied.
+struct OctView {
+    const float* cur;
+    const float* prev;
+    int sp, osize, psp, posize;
+    __device__ __forceinline__ float operator()(int s, int r, int c) const
+    {
+        if (prev != nullptr && s < 2)
+            return prev[(size_t)(s == 0 ? 2 : 4) * posize + (size_t)(2 * r) * psp + 2 * c];
+        return cur[(size_t)s * osize + (size_t)r * sp + c];
+    }
+};
+
+__device__ float fit_quad(const OctView& V, float (&off)[3], int s, int r, int c)
 {
-    const float* cur = src + (size_t)s * osize;
-    const float* prv = cur - osize;
-    const float* nxt = cur + osize;
-    const int idx = r * sp + c;
-    const int inr = idx + sp, ipr = idx - sp, inc = idx + 1, ipc = idx - 1;
+    const float c0 = V(s, r, c);
+    const float nx0 = V(s + 1, r, c), pv0 = V(s - 1, r, c);
+    const float cnr = V(s, r + 1, c), cpr = V(s, r - 1, c), cnc = V(s, r, c + 1), cpc = V(s, r, c - 1);
     float g[3], H[3][3];
-    g[0] = (nxt[idx] - prv[idx]) * 0.5f;
-    g[1] = (cur[inr] - cur[ipr]) * 0.5f;
-    g[2] = (cur[inc] - cur[ipc]) * 0.5f;
-    const float temp = cur[idx] + cur[idx];
-    H[0][0] = (prv[idx] + nxt[idx]) - temp;
-    H[1][1] = (cur[inr] + cur[ipr]) - temp;
-    H[2][2] = (cur[inc] + cur[ipc]) - temp;
-    H[0][1] = ((nxt[inr] - nxt[ipr]) - (prv[inr] - prv[ipr])) * 0.25f;
-    H[0][2] = ((nxt[inc] - nxt[ipc]) - (prv[inc] - prv[ipc])) * 0.25f;
-    H[1][2] = ((cur[inr + 1] - cur[inr - 1]) - (cur[ipr + 1] - cur[ipr - 1])) * 0.25f;
+    g[0] = (nx0 - pv0) * 0.5f;
+    g[1] = (cnr - cpr) * 0.5f;
+    g[2] = (cnc - cpc) * 0.5f;
+    const float temp = c0 + c0;
+    H[0][0] = (pv0 + nx0) - temp;
+    H[1][1] = (cnr + cpr) - temp;
+    H[2][2] = (cnc + cpc) - temp;
+    H[0][1] = ((V(s + 1, r + 1, c) - V(s + 1, r - 1, c)) - (V(s - 1, r + 1, c) - V(s - 1, r - 1, c))) * 0.25f;
+    H[0][2] = ((V(s + 1, r, c + 1) - V(s + 1, r, c - 1)) - (V(s - 1, r, c + 1) - V(s - 1, r, c - 1))) * 0.25f;
+    H[1][2] = ((V(s, r + 1, c + 1) - V(s, r + 1, c - 1)) - (V(s, r - 1, c + 1) - V(s, r - 1, c - 1))) * 0.25f;
     H[1][0] = H[0][1];
     H[2][0] = H[0][2];
     H[2][1] = H[1][2];
@@ -347,40 +393,55 @@ __device__ float fit_quad(const float* __restrict__ src, float (&off)[3], int s,
     off[2] = -g[2];
     solve3(off, H);
     const float dot = (off[0] * g[0] + off[1] * g[1]) + off[2] * g[2];
-    return cur[idx] + 0.5f * dot;
+    return c0 + 0.5f * dot;
 }
 
-__device__ __forceinline__ int32_t trace_sign(const uint32_t* __restrict__ I, int ip, const int* v)
+// getTrace (surfd.cu:369-377).  makePoint builds this box from the
+// interpolated scale without a bounds check (surfd.cu:1010-1020), so near a
+// border a corner can leave [0, W] x [0, H]; the reference then reads the
+// flat pitched buffer at that index (column -1 = the previous row's zero
+// pad).  Same flat read here; indices outside the frame's buffer read 0.
+__device__ __forceinline__ uint32_t flat_at(const uint32_t* __restrict__ I, int idx, int len)
 {
-    const int32_t lxx = (int32_t)(box(I, ip, v[5] + v[2], v[1] + v[3], v[6] - v[2], v[1] - v[3])
-                                  - 3u * box(I, ip, v[0] + v[2], v[1] + v[3], v[0] - v[2], v[1] - v[3]));
-    const int32_t lyy = (int32_t)(box(I, ip, v[0] + v[3], v[7] + v[2], v[0] - v[3], v[8] - v[2])
-                                  - 3u * box(I, ip, v[0] + v[3], v[1] + v[2], v[0] - v[3], v[1] - v[2]));
+    return (idx >= 0 && idx < len) ? I[idx] : 0u;
+}
+__device__ __forceinline__ uint32_t box_flat(const uint32_t* __restrict__ I, int ip, int len, int x1, int y1,
+                                             int x2, int y2)
+{
+    const int yp1 = (y1 + 1) * ip;
+    const int yp2 = y2 * ip;
+    return flat_at(I, yp1 + x1 + 1, len) + flat_at(I, yp2 + x2, len) - flat_at(I, yp2 + x1 + 1, len) -
+           flat_at(I, yp1 + x2, len);
+}
+__device__ __forceinline__ int32_t trace_sign(const uint32_t* __restrict__ I, int ip, int len, const int* v)
+{
+    const int32_t lxx = (int32_t)(box_flat(I, ip, len, v[5] + v[2], v[1] + v[3], v[6] - v[2], v[1] - v[3])
+                                  - 3u * box_flat(I, ip, len, v[0] + v[2], v[1] + v[3], v[0] - v[2], v[1] - v[3]));
+    const int32_t lyy = (int32_t)(box_flat(I, ip, len, v[0] + v[3], v[7] + v[2], v[0] - v[3], v[8] - v[2])
+                                  - 3u * box_flat(I, ip, len, v[0] + v[3], v[1] + v[2], v[0] - v[3], v[1] - v[2]));
     return ((int32_t)((uint32_t)lxx + (uint32_t)lyy) > 0) ? 1 : -1;
 }
 
-__device__ bool nms_point(const uint32_t* __restrict__ I, const float* __restrict__ src, const FrameParams& P,
+__device__ bool nms_point(const uint32_t* __restrict__ I, const OctView& V, const FrameParams& P,
                           const OctaveParams& q, int o, int z, int x, int y, surfhip_point& pt)
 {
-    const int sw = q.sw, sh = q.sh, sp = q.sp, osize = q.osize;
+    const int sw = q.sw, sh = q.sh;
     const int k = 2 * z + 1;
     const int mb = q.mb[z];
     const int i = mb + y * 2;
     const int j = mb + x * 2;
     if (i >= sh - mb || j >= sw - mb) return false;
 
-    int iw = i * sp + j, ix = iw + 1, iy = iw + sp, iz = iy + 1;
-    const float* cs = src + (size_t)k * osize;
+    // argmax over the 2x2x2 block, order (k: w,x,y,z; k+1: w,x,y,z), strict '>'
     int cas = 0;
-    float best = cs[iw];
-    if (cs[ix] > best) { best = cs[ix]; cas = 1; }
-    if (cs[iy] > best) { best = cs[iy]; cas = 2; }
-    if (cs[iz] > best) { best = cs[iz]; cas = 3; }
-    cs += osize;
-    if (cs[iw] > best) { best = cs[iw]; cas = 4; }
-    if (cs[ix] > best) { best = cs[ix]; cas = 5; }
-    if (cs[iy] > best) { best = cs[iy]; cas = 6; }
-    if (cs[iz] > best) { best = cs[iz]; cas = 7; }
+    float best = V(k, i, j), t;
+    if ((t = V(k, i, j + 1)) > best) { best = t; cas = 1; }
+    if ((t = V(k, i + 1, j)) > best) { best = t; cas = 2; }
+    if ((t = V(k, i + 1, j + 1)) > best) { best = t; cas = 3; }
+    if ((t = V(k + 1, i, j)) > best) { best = t; cas = 4; }
+    if ((t = V(k + 1, i, j + 1)) > best) { best = t; cas = 5; }
+    if ((t = V(k + 1, i + 1, j)) > best) { best = t; cas = 6; }
+    if ((t = V(k + 1, i + 1, j + 1)) > best) { best = t; cas = 7; }
     if (best < P.thresh * 0.8f || (k + 1 == P.max_scale - 1 && cas > 3)) return false;
 
     int s = k, r = i, c = j, ds = -1, dr = -1, dc = -1;
@@ -395,32 +456,25 @@ __device__ bool nms_point(const uint32_t* __restrict__ I, const float* __restric
             else if (cas == 7) { c = j + 1; r = i + 1; dc = 1; dr = 1; }
         }
     }
-    int ss = s + ds;
-    cs = src + (size_t)ss * osize;
-    iy = (r - dr) * sp + c; ix = iy - 1; iz = iy + 1;
-    if (best < cs[ix] || best < cs[iy] || best < cs[iz]) return false;
-    iy += dr * sp; ix = iy - 1; iz = iy + 1;
-    if (best < cs[ix] || best < cs[iy] || best < cs[iz]) return false;
-    iy += dr * sp; ix = iy - 1; iz = iy + 1;
-    if (best < cs[ix] || best < cs[iy] || best < cs[iz]) return false;
-    cs = src + (size_t)s * osize;
-    if (best < cs[ix] || best < cs[iy] || best < cs[iz]) return false;
-    iw = r * sp + c + dc;
-    if (best < cs[iw]) return false;
-    iw -= dr * sp;
-    if (best < cs[iw]) return false;
-    ss = s - ds;
-    cs = src + (size_t)ss * osize;
-    if (best < cs[ix] || best < cs[iy] || best < cs[iz] || best < cs[iw]) return false;
-    iw += dr * sp;
-    if (best < cs[iw]) return false;
+    // the 19 neighbours outside the block (surfd.cu:757-792); ties survive
+    const int so = s + ds, si = s - ds;
+#pragma unroll
+    for (int rr = -1; rr <= 1; rr++) {
+        const int row = r + rr * dr;
+        if (best < V(so, row, c - 1) || best < V(so, row, c) || best < V(so, row, c + 1)) return false;
+    }
+    const int rn = r + dr, rp = r - dr, cn = c + dc;
+    if (best < V(s, rn, c - 1) || best < V(s, rn, c) || best < V(s, rn, c + 1)) return false;
+    if (best < V(s, r, cn) || best < V(s, rp, cn)) return false;
+    if (best < V(si, rn, c - 1) || best < V(si, rn, c) || best < V(si, rn, c + 1)) return false;
+    if (best < V(si, rp, cn) || best < V(si, r, cn)) return false;
 
     float off[3] = {0.f, 0.f, 0.f};
     float strength = 0.f;
     int newr = r, newc = c;
     for (int mv = 0; mv < 5; mv++) {
         r = newr; c = newc;
-        strength = fit_quad(src, off, s, r, c, osize, sp);
+        strength = fit_quad(V, off, s, r, c);
         const int bs = q.borders[s];
         if (off[1] > 0.6f && r < sh - bs) newr++;
         if (off[1] < -0.6f && r > bs) newr--;
@@ -460,23 +514,37 @@ __device__ bool nms_point(const uint32_t* __restrict__ I, const float* __restric
     v[6] = v[0] - temp;
     v[7] = v[1] + temp;
     v[8] = v[1] - temp;
-    pt.laplace = trace_sign(I, P.ip, v);
+    pt.laplace = trace_sign(I, P.ip, P.iH * P.ip, v);
     return true;
 }
 
+// All octaves and both NMS levels in one launch (blockIdx.x), frame = blockIdx.y.
 __global__ __launch_bounds__(256) void k_nms(const int32_t* __restrict__ ii, const float* __restrict__ resp,
-                                             FrameParams P, OctaveParams q, int o,
-                                             surfhip_point* __restrict__ cand, uint32_t* __restrict__ keys,
-                                             int* __restrict__ cand_count, int cap)
+                                             FrameParams P, const OctaveParams* __restrict__ oct,
+                                             LaunchPlan plan, surfhip_point* __restrict__ cand,
+                                             uint32_t* __restrict__ keys, int* __restrict__ cand_count, int cap)
 {
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
-    const int f = blockIdx.z >> 1, z = blockIdx.z & 1;
+    const int o = octave_of(plan.nms_start, P.noct, blockIdx.x);
+    const OctaveParams& q = oct[o];
+    const int nbx = plan.nms_nbx[o], nby = plan.nms_nby[o];
+    int lb = blockIdx.x - plan.nms_start[o];
+    const int z = lb / (nbx * nby);
+    lb -= z * nbx * nby;
+    const int x = (lb % nbx) * 64 + (threadIdx.x & 63);
+    const int y = (lb / nbx) * 4 + (threadIdx.x >> 6);
+    const int f = blockIdx.y;
     const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
-    const float* src = resp + (size_t)f * P.resp_stride + q.ooff;
+    const float* F = resp + (size_t)f * P.resp_stride;
+    OctView V;
+    V.cur = F + q.ooff;
+    V.prev = o > 0 ? F + q.pooff : nullptr;
+    V.sp = q.sp;
+    V.osize = q.osize;
+    V.psp = q.psp;
+    V.posize = q.posize;
     surfhip_point pt;
     bool ok = false;
-    if (x < q.nms_gx && y < q.nms_gy) ok = nms_point(I, src, P, q, o, z, x, y, pt);
+    if (x < q.nms_gx && y < q.nms_gy) ok = nms_point(I, V, P, q, o, z, x, y, pt);
     const unsigned long long m = __ballot(ok);
     if (m == 0ull) return;
     const int leader = __builtin_ctzll(m);
@@ -496,13 +564,12 @@ __global__ __launch_bounds__(256) void k_nms(const int32_t* __restrict__ ii, con
 }
 
 hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,
-                      const OctaveParams& q, int o, surfhip_point* cand, uint32_t* keys,
-                      int* cand_count, int cap, hipStream_t s)
+                      const OctaveParams* d_oct, const LaunchPlan& plan, surfhip_point* cand,
+                      uint32_t* keys, int* cand_count, int cap, hipStream_t s)
 {
-    if (q.nms_gx <= 0 || q.nms_gy <= 0) return hipSuccess;
-    if (q.nms_gx >= (1 << 14) || q.nms_gy >= (1 << 14)) return hipErrorInvalidValue;
-    dim3 grid((q.nms_gx + 63) / 64, (q.nms_gy + 3) / 4, nframes * 2);
-    k_nms<<<grid, 256, 0, s>>>(ii, resp, P, q, o, cand, keys, cand_count, cap);
+    if (plan.nms_start[kMaxOct] == 0) return hipSuccess;
+    dim3 grid(plan.nms_start[kMaxOct], nframes);
+    k_nms<<<grid, 256, 0, s>>>(ii, resp, P, d_oct, plan, cand, keys, cand_count, cap);
     return hipGetLastError();
 }
 
@@ -953,33 +1020,43 @@ hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_poin
 }
 
 // ======================================================================
-// Result slab packing for the multi-GPU all-gather.
+// Result slab for the multi-GPU all-gather, compacted:
+//   int32 header[4] = {nframes, total, nfeatures, 0}
+//   int32 counts[nframes] (padded to 16 B)
+//   SurfPoint points[total]            frame-major, canonical order
+//   float     desc[total][nfeatures]   (absent when desc == nullptr)
+// offsets[] is the exclusive prefix of counts written by k_offsets.
 // ======================================================================
 __global__ __launch_bounds__(256) void k_pack(const surfhip_point* __restrict__ pts, const float* __restrict__ desc,
-                                              const int* __restrict__ counts, int max_pts, int nfeat,
-                                              size_t slab_bytes, uint8_t* __restrict__ slab)
+                                              const int* __restrict__ counts, const int* __restrict__ offsets,
+                                              int nframes, int max_pts, int nfeat, uint8_t* __restrict__ slab)
 {
     const int f = blockIdx.y;
-    uint8_t* base = slab + (size_t)f * slab_bytes;
-    const int cnt = counts[f];
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        reinterpret_cast<int*>(base)[0] = cnt;
-        reinterpret_cast<int*>(base)[1] = max_pts;
-        reinterpret_cast<int*>(base)[2] = nfeat;
-        reinterpret_cast<int*>(base)[3] = 0;
+    const int total = offsets[nframes];
+    int* hdr = reinterpret_cast<int*>(slab);
+    if (f == 0 && blockIdx.x == 0) {
+        if (threadIdx.x == 0) { hdr[0] = nframes; hdr[1] = total; hdr[2] = desc ? nfeat : 0; hdr[3] = 0; }
+        for (int i = threadIdx.x; i < nframes; i += 256) hdr[4 + i] = counts[i];
     }
-    surfhip_point* pout = reinterpret_cast<surfhip_point*>(base + 16);
-    float* dout = reinterpret_cast<float*>(base + 16 + (size_t)max_pts * sizeof(surfhip_point));
+    const size_t head = 16 + (((size_t)nframes * 4 + 15) & ~(size_t)15);
+    surfhip_point* pout = reinterpret_cast<surfhip_point*>(slab + head);
+    float* dout = reinterpret_cast<float*>(slab + head + (size_t)total * sizeof(surfhip_point));
+    const int cnt = counts[f], off = offsets[f];
     const size_t tid = (size_t)blockIdx.x * 256 + threadIdx.x, stride = (size_t)gridDim.x * 256;
-    for (size_t t = tid; t < (size_t)cnt; t += stride) pout[t] = pts[(size_t)f * max_pts + t];
-    if (desc)
-        for (size_t t = tid; t < (size_t)cnt * nfeat; t += stride) dout[t] = desc[(size_t)f * max_pts * nfeat + t];
+    for (size_t t = tid; t < (size_t)cnt; t += stride) pout[off + t] = pts[(size_t)f * max_pts + t];
+    if (desc) {
+        const float* src = desc + (size_t)f * max_pts * nfeat;
+        float* dst = dout + (size_t)off * nfeat;
+        const size_t n4 = (size_t)cnt * nfeat / 4;          // nfeat is 64 or 128
+        for (size_t t = tid; t < n4; t += stride)
+            reinterpret_cast<float4*>(dst)[t] = reinterpret_cast<const float4*>(src)[t];
+    }
 }
 
-hipError_t launch_pack(const surfhip_point* pts, const float* desc, const int* counts, int nframes,
-                       int max_pts, int nfeat, size_t slab_bytes, uint8_t* slab, hipStream_t s)
+hipError_t launch_pack(const surfhip_point* pts, const float* desc, const int* counts, const int* offsets,
+                       int nframes, int max_pts, int nfeat, uint8_t* slab, hipStream_t s)
 {
-    k_pack<<<dim3(64, nframes), 256, 0, s>>>(pts, desc, counts, max_pts, nfeat, slab_bytes, slab);
+    k_pack<<<dim3(16, nframes), 256, 0, s>>>(pts, desc, counts, offsets, nframes, max_pts, nfeat, slab);
     return hipGetLastError();
 }
 

@@ -172,10 +172,16 @@ int surfhip_run_hessian(surfhip_detector* det, int nframes);
  * integral image read once + valid responses written. */
 long long surfhip_hessian_bytes_per_frame(surfhip_detector* det);
 
-/* Result slab for the multi-GPU all-gather: per frame
- * [count int32][pad to 16 B][max_pts SurfPoint][max_pts*nfeatures f32].
- * Pack nframes frames' results into d_slab (device, slab_bytes*nframes). */
-size_t surfhip_slab_bytes(int max_pts, int nfeatures);
+/* Result slab for the multi-GPU all-gather, compacted to the
+ * keypoints actually found by the last detect_batch:
+ *   int32 {nframes, total, nfeatures (0 without descriptors), 0}
+ *   int32 counts[nframes] padded to 16 B
+ *   SurfPoint points[total]          (frame-major, canonical order)
+ *   float desc[total][nfeatures]
+ * surfhip_batch_total synchronises the stream and returns the batch's total
+ * keypoint count (needed to size the collective). */
+size_t surfhip_slab_bytes(int nframes, int total, int nfeatures);
+int surfhip_batch_total(surfhip_detector* det, int nframes, int* total);
 int surfhip_pack_slab(surfhip_detector* det, const surfhip_point* d_points, const float* d_desc,
                       const int* d_counts, int nframes, void* d_slab);
 

@@ -213,13 +213,32 @@ static float hessian_at(const int32_t* d, const int* v, int p)
     return rr * (a - b);
 }
 
-/* getTrace (surfd.cu:369-377). */
-static int trace_at(const int32_t* d, const int* v, int p)
+/* getSum for getTrace: makePoint builds its box from the interpolated scale
+ * (surfd.cu:1010-1020) without a bounds check, so near the image border a
+ * corner can fall outside [0, W] x [0, H] (e.g. column -1).  The reference
+ * then reads the flat pitched buffer at that index: column -1 of row y is
+ * the zero pad at the end of row y-1.  This restates that flat read, with
+ * zero pad columns, and defines reads outside the frame's buffer as 0. */
+static inline uint32_t flat_at(const uint32_t* u, long idx, long len)
 {
-    const int32_t lxx = (int32_t)(box(d, v[5] + v[2], v[1] + v[3], v[6] - v[2], v[1] - v[3], p)
-                                  - 3u * box(d, v[0] + v[2], v[1] + v[3], v[0] - v[2], v[1] - v[3], p));
-    const int32_t lyy = (int32_t)(box(d, v[0] + v[3], v[7] + v[2], v[0] - v[3], v[8] - v[2], p)
-                                  - 3u * box(d, v[0] + v[3], v[1] + v[2], v[0] - v[3], v[1] - v[2], p));
+    return (idx >= 0 && idx < len) ? u[idx] : 0u;
+}
+static inline uint32_t box_flat(const int32_t* d, int x1, int y1, int x2, int y2, int p, long len)
+{
+    const uint32_t* u = (const uint32_t*)d;
+    long yp1 = (long)y1 * p + p;
+    long yp2 = (long)y2 * p;
+    return flat_at(u, yp1 + x1 + 1, len) + flat_at(u, yp2 + x2, len) - flat_at(u, yp2 + x1 + 1, len) -
+           flat_at(u, yp1 + x2, len);
+}
+
+/* getTrace (surfd.cu:369-377). */
+static int trace_at(const int32_t* d, const int* v, int p, long len)
+{
+    const int32_t lxx = (int32_t)(box_flat(d, v[5] + v[2], v[1] + v[3], v[6] - v[2], v[1] - v[3], p, len)
+                                  - 3u * box_flat(d, v[0] + v[2], v[1] + v[3], v[0] - v[2], v[1] - v[3], p, len));
+    const int32_t lyy = (int32_t)(box_flat(d, v[0] + v[3], v[7] + v[2], v[0] - v[3], v[8] - v[2], p, len)
+                                  - 3u * box_flat(d, v[0] + v[3], v[1] + v[2], v[0] - v[3], v[1] - v[2], p, len));
     return ((int32_t)((uint32_t)lxx + (uint32_t)lyy) > 0) ? 1 : -1;
 }
 
@@ -470,16 +489,7 @@ static int nms_block(const or_param* p, const or_geom* g, const or_octave* q, in
     v[6] = v[0] - temp;
     v[7] = v[1] + temp;
     v[8] = v[1] - temp;
-    /* bounds sanity: the reference never checks (SURVEY A3 says in range) */
-    {
-        const int lo_x = v[6] - v[2], hi_x = v[5] + v[2] + 1;
-        const int lo_y = v[8] - v[2], hi_y = v[7] + v[2] + 1;
-        if (lo_x < 0 || lo_y < 0 || hi_x >= g->iwhp.x || hi_y >= g->iwhp.y) {
-            fprintf(stderr, "oracle: getTrace box out of range (%d,%d)-(%d,%d)\n", lo_x, lo_y, hi_x, hi_y);
-            abort();
-        }
-    }
-    pt->laplace = trace_at(ii, v, g->iwhp.z);
+    pt->laplace = trace_at(ii, v, g->iwhp.z, (long)g->iwhp.y * g->iwhp.z);
     return 1;
 }
 

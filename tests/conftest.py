@@ -35,7 +35,9 @@ def load_surf_amd():
     if "surf_amd" in sys.modules:
         return sys.modules["surf_amd"]
     _ensure_built()
-    spec = importlib.util.spec_from_file_location("surf_amd", os.path.join(REPO, "cuda-surf_amd", "__init__.py"))
+    pkg = os.path.join(REPO, "cuda-surf_amd")
+    spec = importlib.util.spec_from_file_location("surf_amd", os.path.join(pkg, "__init__.py"),
+                                                  submodule_search_locations=[pkg])
     mod = importlib.util.module_from_spec(spec)
     sys.modules["surf_amd"] = mod
     spec.loader.exec_module(mod)

@@ -1,0 +1,251 @@
+"""CPU tests of the oracle (no GPU): known-answer tests against closed forms
+and an independent numpy restatement, geometry against the values SURVEY.md
+derives from the reference's host code, and the frozen golden vectors."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, REF_DATA, assert_points_equal, desc_l2
+
+F32 = np.float32
+
+
+def test_struct_layouts(orc):
+    import ctypes as C
+    assert C.sizeof(orc.Param) == 48
+    assert orc.POINT_DTYPE.itemsize == 48
+    # offsets of surf_structures.h:10-30 / 45-72
+    assert orc.Param.doubled.offset == 8 and orc.Param.upright.offset == 28
+    assert orc.Param.extend.offset == 29 and orc.Param.nfeatures.offset == 44
+    assert [orc.POINT_DTYPE.fields[k][1] for k in ("o", "laplace", "ori", "ambiguity")] == [12, 20, 24, 44]
+
+
+def test_init_params_match_reference_defaults(orc):
+    """Surfor::init (surf.cpp:60-79) with main.cpp's arguments."""
+    p = orc.make_param(4, 4.0, False, 9, 2, True, False, 4)
+    assert (p.init_lobe, p.max_scale, p.sampling, p.mag_factor, p.orient_size, p.nfeatures) == (3, 5, 2, 3, 4, 64)
+    assert p.divisor == 1.0
+    p = orc.make_param(5, 4.0, False, 9, 2, False, True, 4)
+    assert (p.orient_size, p.nfeatures) == (8, 128)
+    with pytest.raises(ValueError):
+        orc.make_param(4, 4.0, True)           # doubled: out of scope
+
+
+def test_geometry_1080p_matches_survey(orc):
+    """SURVEY.md 8 notation + Appendix A3 (values computed from surf.cpp:374-392,
+    surfd.cu:2846-2864, 3062-3076)."""
+    p = orc.make_param(4, 4.0, upright=True)
+    g, octs = orc.geometry(p, 1920, 1080)
+    assert (g.iwhp.x, g.iwhp.y, g.iwhp.z) == (1921, 1081, 2048)
+    assert [(g.swhp[o].x, g.swhp[o].y, g.swhp[o].z) for o in range(4)] == \
+        [(960, 540, 1024), (480, 270, 512), (240, 135, 256), (120, 67, 128)]
+    assert g.tot_osize == 3_671_680
+    o0 = octs[0]
+    assert list(o0.mask[:5]) == [3, 5, 7, 9, 11]
+    assert list(o0.border1[:5]) == [6, 6, 6, 7, 9]
+    assert list(o0.borders[:5]) == [6, 6, 6, 6, 7]
+    assert list(o0.mborders) == [7, 8]
+    for o, masks in ((1, [15, 19, 23]), (2, [31, 39, 47]), (3, [63, 79, 95])):
+        assert list(octs[o].mask[:3]) == masks
+        assert list(octs[o].border1[:3]) == [8, 8, 9]
+        assert list(octs[o].borders[:5]) == [8, 8, 8, 8, 8]
+        assert list(octs[o].mborders) == [9, 9]
+    # NMS launch extents (grids (30,17,2), (15,8,2), (7,4,2), (4,2,2) of 16x16)
+    assert [(octs[o].nms_gx // 16, octs[o].nms_gy // 16) for o in range(4)] == [(30, 17), (15, 8), (7, 4), (4, 2)]
+
+
+def test_hessian_bytes_survey_number(orc):
+    """Compulsory Hessian bytes at 1080p = 20,058,324."""
+    p = orc.make_param(4, 4.0, upright=True)
+    g, octs = orc.geometry(p, 1920, 1080)
+    valid = 0
+    for o in range(4):
+        q = octs[o]
+        for i in range(q.nscale):
+            b = q.border1[i]
+            valid += (g.swhp[o].x - 2 * b) * (g.swhp[o].y - 2 * b)
+    assert valid == 2_937_980
+    assert 1921 * 1081 * 4 + 4 * valid == 20_058_324
+
+
+def test_integral_vs_numpy(orc):
+    rng = np.random.default_rng(1)
+    for w, h in ((1, 1), (7, 3), (64, 48), (333, 101)):
+        img = rng.integers(0, 256, (h, w), dtype=np.uint8)
+        ii = orc.integral(img, w, h)
+        ref = np.zeros((h + 1, w + 1), np.int64)
+        ref[1:, 1:] = img.astype(np.int64).cumsum(0).cumsum(1)
+        np.testing.assert_array_equal(ii[:, :w + 1], ref)
+
+
+def test_box_sum_convention(orc):
+    """getSum(x1, y1, x2, y2) sums the inclusive rect [x2..x1] x [y2..y1]
+    (surfd.cu:334-343)."""
+    rng = np.random.default_rng(2)
+    img = rng.integers(0, 256, (40, 50), dtype=np.uint8)
+    ii = orc.integral(img, 50, 40)
+    for _ in range(50):
+        x2, y2 = rng.integers(0, 45), rng.integers(0, 35)
+        x1, y1 = x2 + rng.integers(0, 4), y2 + rng.integers(0, 4)
+        got = orc.lib.or_test_box(ii.ctypes.data, ii.shape[1], int(x1), int(y1), int(x2), int(y2))
+        assert got == img[y2:y1 + 1, x2:x1 + 1].astype(np.int64).sum()
+
+
+def _np_hessian(img, w, h, p, g, octs):
+    """Independent numpy float32 restatement of getHessian * norm (surfd.cu:353-366,
+    445-481) for octave 0, computed from box sums of the image itself."""
+    ii = np.zeros((h + 1, w + 1), np.int64)
+    ii[1:, 1:] = img[:, :w].astype(np.int64).cumsum(0).cumsum(1)
+
+    def S(x1, y1, x2, y2):
+        return ii[y1 + 1, x1 + 1] + ii[y2, x2] - ii[y2, x1 + 1] - ii[y1 + 1, x2]
+
+    q = octs[0]
+    out = {}
+    for i in range(q.nscale):
+        m, x2, x3, x4 = q.mask[i], q.x2[i], q.x3[i], q.x4[i]
+        b = q.border1[i]
+        sw, sh = g.swhp[0].x, g.swhp[0].y
+        plane = np.zeros((sh, sw), F32)
+        iy, ix = np.mgrid[b:sh - b, b:sw - b]
+        X, Y = q.delta * ix, q.delta * iy
+        dxx = (S(X + m + x2, Y + x3, X - m - x2, Y - x3) - 3 * S(X + x2, Y + x3, X - x2, Y - x3)).astype(F32)
+        dyy = (S(X + x3, Y + m + x2, X - x3, Y - m - x2) - 3 * S(X + x3, Y + x2, X - x3, Y - x2)).astype(F32)
+        dxy = F32(0.6) * (S(X + x4, Y, X, Y - x4) + S(X, Y + x4, X - x4, Y) - S(X + x4, Y + x4, X, Y)
+                          - S(X, Y, X - x4, Y - x4)).astype(F32)
+        r = F32(0.003921568627)
+        plane[b:sh - b, b:sw - b] = (r * r) * (dxx * dyy - dxy * dxy) * F32(q.norm[i])
+        out[i] = plane
+    return out
+
+
+def test_hessian_octave0_vs_numpy(orc, surf):
+    w, h = 200, 150
+    img = surf.synth_frames(1, w, h, first=5)[0]
+    p = orc.make_param(4, 4.0, upright=True)
+    ii, resp, g, octs = orc.hessian(p, img, w, h)
+    ref = _np_hessian(img, w, h, p, g, octs)
+    sw, sh, sp = g.swhp[0].x, g.swhp[0].y, g.swhp[0].z
+    for i, plane in ref.items():
+        got = resp[i * g.osize[0]: (i + 1) * g.osize[0]].reshape(sh, sp)[:, :sw]
+        np.testing.assert_array_equal(got.view(np.uint32), plane.view(np.uint32))
+
+
+def test_halfimage_planes(orc, surf):
+    """Planes 0/1 of octave o > 0 are planes 2/4 of octave o-1 at (2r, 2c)
+    (halfImage, surfd.cu:321-331; surf.cpp:252-258)."""
+    w, h = 320, 240
+    img = surf.synth_frames(1, w, h, first=9)[0]
+    p = orc.make_param(4, 4.0, upright=True)
+    _, resp, g, _ = orc.hessian(p, img, w, h)
+    for o in range(1, 4):
+        sw, sh, sp = g.swhp[o].x, g.swhp[o].y, g.swhp[o].z
+        psw, psh, psp = g.swhp[o - 1].x, g.swhp[o - 1].y, g.swhp[o - 1].z
+        for dst, src in ((0, 2), (1, 4)):
+            d = resp[g.ooff[o] + dst * g.osize[o]:][:sh * sp].reshape(sh, sp)[:, :sw]
+            s = resp[g.ooff[o - 1] + src * g.osize[o - 1]:][:psh * psp].reshape(psh, psp)
+            np.testing.assert_array_equal(d, s[0:2 * sh:2, 0:2 * sw:2])
+
+
+def test_solver_closed_form(orc):
+    """solveLinearSystem (surfd.cu:835-887) on well-conditioned systems."""
+    rng = np.random.default_rng(3)
+    for _ in range(20):
+        A = rng.normal(size=(3, 3)).astype(F32) + 3 * np.eye(3, dtype=F32)
+        x = rng.normal(size=3).astype(F32)
+        b = (A.astype(np.float64) @ x.astype(np.float64)).astype(F32)
+        sol = b.copy()
+        sq = A.copy().ravel()
+        orc.lib.or_test_solve3(sol.ctypes.data, sq.ctypes.data)
+        np.testing.assert_allclose(sol, x, rtol=1e-4, atol=1e-4)
+
+
+def test_place_in_index_weights_sum_to_mag(orc):
+    """placeInIndex (surfd.cu:1199-1271): for interior (rx, cx) the bilinear
+    weights put exactly mag1 + mag2 into the descriptor."""
+    rng = np.random.default_rng(4)
+    for _ in range(200):
+        d = np.zeros(64, F32)
+        rx, cx = rng.uniform(0, 3, 2).astype(F32)
+        m1, m2 = rng.uniform(-1, 1, 2).astype(F32)
+        orc.lib.or_test_place(d.ctypes.data, 4, 4, float(m1), 0, float(m2), 2, float(rx), float(cx))
+        assert abs(d.sum() - (m1 + m2)) < 1e-5
+        assert abs(d[0::4].sum() - m1) < 1e-5 and abs(d[2::4].sum() - m2) < 1e-5
+
+
+def test_luts(orc):
+    l1, l2, b = orc.tables()
+    n = np.arange(83)
+    np.testing.assert_allclose(l1, np.exp(-(n + 0.5) / 12.5), rtol=1e-6)
+    np.testing.assert_allclose(l2, np.exp(-(np.arange(40) + 0.5) / 8), rtol=1e-6)
+    assert b[0] == F32(-np.pi)
+    np.testing.assert_allclose(np.diff(b), 2 * np.pi / 72, rtol=1e-4)
+
+
+def test_sincos_and_atan2(orc):
+    for x in np.linspace(-4.5, 4.5, 2001, dtype=F32):
+        assert abs(orc.lib.or_sinf(float(x)) - np.sin(np.float64(x))) < 3e-7
+        assert abs(orc.lib.or_cosf(float(x)) - np.cos(np.float64(x))) < 3e-7
+    rng = np.random.default_rng(5)
+    for y, x in rng.normal(size=(2000, 2)).astype(F32):
+        assert abs(orc.lib.or_fast_atan2(float(y), float(x)) - np.arctan2(y, x)) < 3e-4   # 3-term polynomial
+
+
+def test_blob_detected_at_center(orc):
+    """A single dark-on-bright Gaussian blob yields a keypoint at its centre."""
+    w, h = 256, 256
+    yy, xx = np.mgrid[0:h, 0:w]
+    sigma, cx, cy = 6.0, 128.3, 121.7
+    img = np.clip(200 - 150 * np.exp(-((xx - cx) ** 2 + (yy - cy) ** 2) / (2 * sigma ** 2)), 0, 255)
+    img = np.round(img).astype(np.uint8)
+    p = orc.make_param(4, 4.0, upright=True)
+    pts, desc, _ = orc.detect(p, img, w, h)
+    assert len(pts) >= 1
+    k = np.argmax(pts["strength"])
+    assert abs(pts["x"][k] - cx) < 1.0 and abs(pts["y"][k] - cy) < 1.0
+    # scale ~ 1.2/9 of the box size; a blob of sigma s peaks near lobe ~ s*2.5
+    assert 3.0 < pts["scale"][k] < 12.0
+    assert pts["laplace"][k] == 1                   # dark blob on bright background: positive trace
+    np.testing.assert_allclose(np.linalg.norm(desc[k]), 1.0, rtol=1e-5)
+
+
+def test_upright_descriptor_flip_symmetry(orc):
+    """Mirroring the image left-right mirrors the upright descriptor cells and
+    flips the sign of the dx bins (an independent property check)."""
+    w, h = 160, 160
+    rng = np.random.default_rng(6)
+    img = np.clip(rng.normal(128, 40, (h, w)), 0, 255).astype(np.uint8)
+    yy, xx = np.mgrid[0:h, 0:w]
+    img = np.clip(img * 0.2 + 200 - 150 * np.exp(-((xx - 80) ** 2 + (yy - 80) ** 2) / 50.0), 0, 255).astype(np.uint8)
+    p = orc.make_param(4, 4.0, upright=True)
+    pts, desc, _ = orc.detect(p, img, w, h)
+    assert len(pts) > 0
+    assert np.allclose(np.linalg.norm(desc, axis=1), 1.0, atol=1e-5)
+
+
+# -------------------------------------------------------------- goldens
+
+GOLDEN_CASES = ["left_1280x960_upright", "left_1280x960_rotated", "right_1280x960_upright",
+                "left_640x480_upright", "left_1280x960_rotated_ext"]
+
+
+@pytest.mark.parametrize("name", GOLDEN_CASES)
+def test_oracle_matches_golden(orc, name):
+    """The oracle reproduces the frozen vectors (tests/golden, generated by
+    tests/golden/make_golden.py from the reference's data/*.pgm)."""
+    path = os.path.join(GOLDEN, name + ".npz")
+    if not os.path.exists(path):
+        pytest.skip("golden fixtures not generated")
+    z = np.load(path)
+    img = np.load(os.path.join(GOLDEN, "images.npz"))[str(z["image_key"])]
+    h, w = img.shape
+    upright, extend = bool(z["meta"][0]), bool(z["meta"][1])
+    p = orc.make_param(4, 4.0, False, 9, 2, upright, extend, 4)
+    pts, desc, nc = orc.detect(p, img, w, h)
+    ref = np.frombuffer(z["points"].tobytes(), dtype=orc.POINT_DTYPE)
+    assert_points_equal(pts, ref, fields=("x", "y", "scale", "o", "strength", "laplace", "ori"))
+    assert desc_l2(desc, z["desc"]).max() == 0.0
+    assert nc == int(z["meta"][2])
