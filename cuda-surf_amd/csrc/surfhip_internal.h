@@ -63,11 +63,14 @@ struct LaunchPlan {
     int hess_nbx[kMaxOct];          // blocks per row of samples
     int nms_start[kMaxOct + 1];     // NMS blocks of octave o (both levels)
     int nms_nbx[kMaxOct], nms_nby[kMaxOct];
+    int o0_lds;                     // octave 0 on the LDS-tiled kernel (k_hess_o0)
+    int o0_nbx, o0_blocks;
 };
 void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan);
 
 hipError_t launch_hessian(const int32_t* ii, float* resp, int nframes, const FrameParams& P,
-                          const OctaveParams* d_oct, const LaunchPlan& plan, hipStream_t s);
+                          const OctaveParams* d_oct, const OctaveParams& q0, const LaunchPlan& plan,
+                          hipStream_t s);
 hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,
                       const OctaveParams* d_oct, const LaunchPlan& plan, surfhip_point* cand,
                       uint32_t* keys, int* cand_count, int cap, hipStream_t s);

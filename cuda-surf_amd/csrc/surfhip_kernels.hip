@@ -252,16 +252,147 @@ __device__ __forceinline__ float hessian_at(const uint32_t* __restrict__ I, int 
     return rr * (a - b);
 }
 
+// ----------------------------------------------------------------------
+// Octave 0 (sampling 2 => 2 px between samples, lobes 3..11): LDS tiles.
+// 85 % of all responses live here and every integral value is re-read ~40
+// times, so a workgroup stages a tile of the integral image in LDS with
+// coalesced 16-B loads and computes 128 x 16 samples x 5 scales from it.
+// Layout: parity planes (even / odd image columns) of *pairs*
+//   T[row][p][k] = (I[row][xs + 2k + p], I[row][xs + 2k + p + 128])
+// so lane l, which owns samples ix and ix + 64 (x0 and x0 + 128 px), gets
+// both samples' corner with ONE conflict-free ds_read_b64 whose offset is a
+// compile-time immediate (the lobe geometry is fixed for init_lobe 3).
+// 64 rows x 2 planes x 80 pairs x 8 B = 80 KiB -> two workgroups per CU.
+// ----------------------------------------------------------------------
+namespace o0 {
+constexpr int TXS = 128;                 // samples per tile row (64 lanes x 2)
+constexpr int TYS = 16;                  // sample rows per tile
+constexpr int NR = 2 * TYS + 32;         // image rows: y0 - 16 .. y0 + 17 over the tile
+constexpr int NK = 80;                   // pairs per parity-plane row
+constexpr int THREADS = 512;
+}
+
+// LDS-qualified volatile view: volatile stops hipcc from pairing neighbouring
+// reads into ds_read2_b64 (half the bandwidth of ds_read_b64 on gfx950);
+// the explicit address space keeps them ds_ (a plain volatile* goes flat_).
+typedef const volatile uint64_t __attribute__((address_space(3))) lds_u64;
+
+template <int M, int X2, int X3, int X4>
+__device__ __forceinline__ void hess_pair(const lds_u64* Tb, float norm, float& ha, float& hb)
+{
+    // corner (dr, dc) relative to (y0, x0); Tb points at row y0 - 16, lane l
+#define C(dr, dc) Tb[((dr) + 16) * 2 * o0::NK + ((dc) & 1) * o0::NK + ((16 + (dc)) >> 1)]
+    const uint64_t a1 = C(X3 + 1, M + X2 + 1), a2 = C(-X3, -M - X2), a3 = C(-X3, M + X2 + 1), a4 = C(X3 + 1, -M - X2);
+    const uint64_t b1 = C(X3 + 1, X2 + 1), b2 = C(-X3, -X2), b3 = C(-X3, X2 + 1), b4 = C(X3 + 1, -X2);
+    const uint64_t c1 = C(M + X2 + 1, X3 + 1), c2 = C(-M - X2, -X3), c3 = C(-M - X2, X3 + 1), c4 = C(M + X2 + 1, -X3);
+    const uint64_t d1 = C(X2 + 1, X3 + 1), d2 = C(-X2, -X3), d3 = C(-X2, X3 + 1), d4 = C(X2 + 1, -X3);
+    const uint64_t s1a = C(1, X4 + 1), s1b = C(-X4, 0), s1c = C(-X4, X4 + 1), s1d = C(1, 0);
+    const uint64_t s2a = C(X4 + 1, 1), s2b = C(0, -X4), s2c = C(0, 1), s2d = C(X4 + 1, -X4);
+    const uint64_t s3a = C(X4 + 1, X4 + 1), s3b = C(0, 0), s3c = C(0, X4 + 1), s3d = C(X4 + 1, 0);
+    const uint64_t s4a = C(1, 1), s4b = C(-X4, -X4), s4c = C(-X4, 1), s4d = C(1, -X4);
+#undef C
+    const float rr = INV255 * INV255;
+#define LO(v) ((uint32_t)(v))
+#define HI(v) ((uint32_t)((v) >> 32))
+#define RESP(F, out)                                                                                  \
+    {                                                                                                 \
+        const uint32_t A = F(a1) + F(a2) - F(a3) - F(a4), B = F(b1) + F(b2) - F(b3) - F(b4);          \
+        const uint32_t Cc = F(c1) + F(c2) - F(c3) - F(c4), D = F(d1) + F(d2) - F(d3) - F(d4);         \
+        const uint32_t S1 = F(s1a) + F(s1b) - F(s1c) - F(s1d), S2 = F(s2a) + F(s2b) - F(s2c) - F(s2d);\
+        const uint32_t S3 = F(s3a) + F(s3b) - F(s3c) - F(s3d), S4 = F(s4a) + F(s4b) - F(s4c) - F(s4d);\
+        const float dxx = (float)(int32_t)(A - 3u * B);                                               \
+        const float dyy = (float)(int32_t)(Cc - 3u * D);                                              \
+        const float dxy = 0.6f * (float)(int32_t)(S1 + S2 - S3 - S4);                                 \
+        const float p = dxx * dyy;                                                                    \
+        const float q2 = dxy * dxy;                                                                   \
+        out = (rr * (p - q2)) * norm;                                                                 \
+    }
+    RESP(LO, ha)
+    RESP(HI, hb)
+#undef RESP
+#undef LO
+#undef HI
+}
+
+template <int S, int M, int X2, int X3, int X4>
+__device__ __forceinline__ void hess_store(const lds_u64* Tb, const OctaveParams& q, float* row, int iy,
+                                           int ixa, int ixb)
+{
+    float ha, hb;
+    hess_pair<M, X2, X3, X4>(Tb, q.norm[S], ha, hb);
+    const int b1 = q.b1[S];
+    const bool vy = iy >= b1 && iy < q.sh - b1;
+    float* pl = row + (size_t)S * q.osize;
+    if (ixa < q.sw) pl[ixa] = (vy && ixa >= b1 && ixa < q.sw - b1) ? ha : 0.f;
+    if (ixb < q.sw) pl[ixb] = (vy && ixb >= b1 && ixb < q.sw - b1) ? hb : 0.f;
+}
+
+__global__ __launch_bounds__(o0::THREADS, 4) void k_hess_o0(const int32_t* __restrict__ ii, float* __restrict__ resp,
+                                                            FrameParams P, OctaveParams q, int nbx)
+{
+    __shared__ __attribute__((aligned(16))) uint64_t T[o0::NR * 2 * o0::NK];
+    const int bx = blockIdx.x % nbx, by = blockIdx.x / nbx, f = blockIdx.y;
+    const int IX0 = bx * o0::TXS, IY0 = by * o0::TYS;
+    const int xs = 2 * IX0 - 16, ys = 2 * IY0 - 16;
+    const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
+    // ---- fill: item (row, a) loads image columns xs+4a.. and xs+4a+128..
+    for (int t = threadIdx.x; t < o0::NR * 40; t += o0::THREADS) {
+        const int ry = t / 40, a = t - ry * 40;
+        const int gy = ys + ry, gx = xs + 4 * a;
+        uint4 g0 = make_uint4(0u, 0u, 0u, 0u), g1 = g0;
+        if (gy >= 0 && gy < P.iH) {
+            const uint32_t* row = I + (size_t)gy * P.ip;
+            if (gx >= 0 && gx < P.ip) g0 = *reinterpret_cast<const uint4*>(row + gx);
+            if (gx + 128 < P.ip) g1 = *reinterpret_cast<const uint4*>(row + gx + 128);
+        }
+        uint64_t* dst = T + ry * 2 * o0::NK + 2 * a;
+        *reinterpret_cast<uint4*>(dst) = make_uint4(g0.x, g1.x, g0.z, g1.z);            // even plane, k = 2a, 2a+1
+        *reinterpret_cast<uint4*>(dst + o0::NK) = make_uint4(g0.y, g1.y, g0.w, g1.w);   // odd plane
+    }
+    __syncthreads();
+    // ---- compute: wave w owns sample rows w, w + 8; lane l samples ix, ix + 64
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int ixa = IX0 + lane, ixb = ixa + 64;
+    float* F = resp + (size_t)f * P.resp_stride + q.ooff;
+    for (int r = w; r < o0::TYS; r += o0::THREADS / 64) {
+        const int iy = IY0 + r;
+        if (iy >= q.sh) break;
+        const lds_u64* Tb = (const lds_u64*)(T + (2 * r) * 2 * o0::NK + lane);    // image row y0 - 16
+        float* row = F + (size_t)iy * q.sp;
+        hess_store<0, 3, 1, 2, 3>(Tb, q, row, iy, ixa, ixb);
+        hess_store<1, 5, 2, 4, 6>(Tb, q, row, iy, ixa, ixb);
+        hess_store<2, 7, 3, 6, 9>(Tb, q, row, iy, ixa, ixb);
+        hess_store<3, 9, 4, 8, 12>(Tb, q, row, iy, ixa, ixb);
+        hess_store<4, 11, 5, 10, 15>(Tb, q, row, iy, ixa, ixb);
+    }
+}
+
+// Octave 0 takes the LDS path when its geometry is the fixed one compiled
+// into k_hess_o0 (sampling 2, lobes 3/5/7/9/11).
+static bool o0_lds_ok(const FrameParams& P, const OctaveParams& q)
+{
+    static const int masks[5] = {3, 5, 7, 9, 11};
+    if (P.sampling != 2 || q.delta != 2 || q.nscale != 5 || q.init_scale != 0) return false;
+    for (int i = 0; i < 5; i++)
+        if (q.mask[i] != masks[i] || q.x2[i] != masks[i] / 2 || q.x3[i] != 2 * (masks[i] / 2) ||
+            q.x4[i] != 3 * (masks[i] / 2))
+            return false;
+    return true;
+}
+
 void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan)
 {
     int hb = 0, nb = 0;
+    plan.o0_lds = P.noct > 0 && o0_lds_ok(P, oct[0]);
+    plan.o0_nbx = (oct[0].sw + o0::TXS - 1) / o0::TXS;
+    plan.o0_blocks = plan.o0_nbx * ((oct[0].sh + o0::TYS - 1) / o0::TYS);
     for (int o = 0; o < kMaxOct; o++) {
         plan.hess_start[o] = hb;
         plan.nms_start[o] = nb;
         if (o < P.noct) {
             const OctaveParams& q = oct[o];
             plan.hess_nbx[o] = (q.sw + 63) / 64;
-            hb += plan.hess_nbx[o] * ((q.sh + 3) / 4);
+            if (!(o == 0 && plan.o0_lds)) hb += plan.hess_nbx[o] * ((q.sh + 3) / 4);
             plan.nms_nbx[o] = (q.nms_gx + 63) / 64;
             plan.nms_nby[o] = (q.nms_gy + 3) / 4;
             nb += 2 * plan.nms_nbx[o] * plan.nms_nby[o];
@@ -310,10 +441,13 @@ __global__ __launch_bounds__(256) void k_hessian(const int32_t* __restrict__ ii,
 }
 
 hipError_t launch_hessian(const int32_t* ii, float* resp, int nframes, const FrameParams& P,
-                          const OctaveParams* d_oct, const LaunchPlan& plan, hipStream_t s)
+                          const OctaveParams* d_oct, const OctaveParams& q0, const LaunchPlan& plan,
+                          hipStream_t s)
 {
-    dim3 grid(plan.hess_start[kMaxOct], nframes);
-    k_hessian<<<grid, 256, 0, s>>>(ii, resp, P, d_oct, plan);
+    if (plan.o0_lds)
+        k_hess_o0<<<dim3(plan.o0_blocks, nframes), o0::THREADS, 0, s>>>(ii, resp, P, q0, plan.o0_nbx);
+    if (plan.hess_start[kMaxOct] > 0)
+        k_hessian<<<dim3(plan.hess_start[kMaxOct], nframes), 256, 0, s>>>(ii, resp, P, d_oct, plan);
     return hipGetLastError();
 }
 

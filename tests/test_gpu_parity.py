@@ -104,7 +104,7 @@ def _plane_views(resp, g, octs, p):
             yield o, s, resp[base:base + sh * sp].reshape(sh, sp)[:, :sw]
 
 
-@pytest.mark.parametrize("w,h", [(640, 480), (1920, 1080)])
+@pytest.mark.parametrize("w,h", [(64, 48), (333, 211), (640, 480), (1920, 1080), (3840, 2160)])
 def test_hessian_planes_bit_exact(surf, orc, w, h):
     frames = surf.synth_frames(1, w, h, first=7)
     param = surf.make_param(4, 4.0, upright=True)
