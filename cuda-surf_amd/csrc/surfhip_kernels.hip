@@ -1143,13 +1143,161 @@ __global__ __launch_bounds__(256) void k_describe(const int32_t* __restrict__ ii
     }
 }
 
+// ----------------------------------------------------------------------
+// Upright descriptor (U-SURF, 4x4 cells), deterministic and atomic-free.
+// The upright sample grid is separable: a sample's cell row (ri, rfrac)
+// depends only on its grid row i and its cell column (ci, cfrac) only on its
+// grid column j (surfd.cu:1290-1294).  So lane = grid column j, the wave
+// walks the rows i (cell row wave-uniform), and each lane accumulates its
+// placeInIndex contributions (surfd.cu:1199-1271) for cell columns ci and
+// ci+1 in registers.  A fixed-order cross-lane reduction through LDS then
+// forms the 16 cells.  Per-sample weights are the reference's exact float
+// products; only the summation order differs from the oracle's (<= 1e-6).
+// iradius <= 22 for wsz 4 (7.5 * scale / step, step = rn(scale / 2)), so the
+// (2 iradius + 1) columns fit one wave.
+// ----------------------------------------------------------------------
+template <bool EXT>
+__global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__ ii, FrameParams P,
+                                                     const surfhip_point* __restrict__ pts, int max_pts,
+                                                     const int* __restrict__ offsets, int nframes,
+                                                     float* __restrict__ desc)
+{
+    constexpr int WSZ = 4;
+    constexpr int NB = EXT ? 8 : 4;                       // bins per cell
+    constexpr int NF = WSZ * WSZ * NB;
+    __shared__ float red[4][2][WSZ][NB][64];              // [wave][k][R][bin][lane]
+    __shared__ int cis[4][64];
+    const unsigned lane = lane_id();
+    const int w = threadIdx.x >> 6;
+    const int total = offsets[nframes];
+    const float fw = (float)WSZ;
+    const float wofs = (float)WSZ * 0.5f - 0.5f;
+    for (int g = blockIdx.x * 4 + w; g < total; g += gridDim.x * 4) {
+        int lo = 0, hi = nframes;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (offsets[mid] <= g) lo = mid; else hi = mid;
+        }
+        const int f = lo, kp = g - offsets[lo];
+        const surfhip_point p = pts[(size_t)f * max_pts + kp];
+        const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
+        const int ip = P.ip;
+        const float scale = 1.65f * p.scale;
+        const int step = max(f2i_rn(scale * 0.5f), 1);
+        const int ix = f2i_rn(p.x), iy = f2i_rn(p.y);
+        const float dx0 = p.x - (float)ix, dy0 = p.y - (float)iy;
+        const float spacing = scale * (float)P.mag;
+        const int hs = f2i_rz(scale);
+        const int rlim = P.iH - 1 - hs, clim = P.W - hs;
+        const int iradius = f2i_rn(((spacing * (float)(WSZ + 1)) * 0.5f) / (float)step);
+        // ---- per-lane column geometry
+        const int sj = (int)lane - iradius;
+        const float cpos = ((float)(step * sj) - dx0) / spacing;
+        const float cx = cpos + wofs;
+        const int c = ix + sj * step;
+        const bool col_on = (int)lane <= 2 * iradius && cx > -1.f && cx < fw && c >= 1 + hs && c < clim;
+        const int ci = f2i_rz(cx >= 0.f ? cx : cx - 1.f);
+        const float cfrac = cx - (float)ci;
+        const float cfrac1 = 1 - cfrac;
+        const bool k0 = col_on && ci >= 0, k1 = col_on && ci + 1 < WSZ;
+        float acc[2][WSZ][NB];
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+#pragma unroll
+            for (int R = 0; R < WSZ; R++)
+#pragma unroll
+                for (int b = 0; b < NB; b++) acc[k][R][b] = 0.f;
+        for (int si = -iradius; si <= iradius; si++) {
+            const float rpos = ((float)(step * si) - dy0) / spacing;
+            const float rx = rpos + wofs;
+            const int r = iy + si * step;
+            if (!(rx > -1.f && rx < fw && r >= 1 + hs && r < rlim)) continue;     // wave-uniform
+            const int ri = f2i_rz(rx >= 0.f ? rx : rx - 1.f);
+            const float rfrac = rx - (float)ri;
+            if (!col_on) continue;
+            const float weight = c_tab.lut2[f2i_rz(rpos * rpos + cpos * cpos)];
+            const float dx = (weight * (float)wavelet2(I, ip, c, r, hs)) * INV255;
+            const float dy = (weight * (float)wavelet1(I, ip, c, r, hs)) * INV255;
+            // the (mag, bin) pairs placeInIndex receives (surfd.cu:1306-1314)
+            float mag[4];
+            int bin[4];
+            if constexpr (!EXT) {
+                mag[0] = dx; bin[0] = dx < 0 ? 0 : 1;
+                mag[1] = dy; bin[1] = dy < 0 ? 2 : 3;
+            } else {
+                mag[0] = dx; bin[0] = dy < 0 ? 0 : 1;
+                mag[1] = fabsf(dx); bin[1] = dy < 0 ? 2 : 3;
+                mag[2] = dy; bin[2] = dx < 0 ? 4 : 5;
+                mag[3] = fabsf(dy); bin[3] = dx < 0 ? 6 : 7;
+            }
+            constexpr int NM = EXT ? 4 : 2;
+#pragma unroll
+            for (int R = 0; R < WSZ; R++) {
+                if (R != ri && R != ri + 1) continue;                             // wave-uniform
+                const float rw = (R == ri) ? (1.f - rfrac) : rfrac;
+#pragma unroll
+                for (int t = 0; t < NM; t++) {
+                    const float rv = mag[t] * rw;
+                    const float v0 = k0 ? rv * cfrac1 : 0.f;
+                    const float v1 = k1 ? rv * cfrac : 0.f;
+                    // mag t always lands in bin 2t or 2t + 1
+                    const bool odd = bin[t] & 1;
+                    acc[0][R][2 * t] += odd ? 0.f : v0;
+                    acc[0][R][2 * t + 1] += odd ? v0 : 0.f;
+                    acc[1][R][2 * t] += odd ? 0.f : v1;
+                    acc[1][R][2 * t + 1] += odd ? v1 : 0.f;
+                }
+            }
+        }
+        // ---- ordered cross-lane reduction into the 16 cells
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+#pragma unroll
+            for (int R = 0; R < WSZ; R++)
+#pragma unroll
+                for (int b = 0; b < NB; b++) red[w][k][R][b][lane] = acc[k][R][b];
+        cis[w][lane] = col_on ? ci : -100;
+        wave_sync();
+        const int nlanes = min(2 * iradius + 1, 64);
+        float v[2];
+#pragma unroll
+        for (int h = 0; h < (NF + 63) / 64; h++) {
+            const int o = (int)lane + 64 * h;            // output index (R * WSZ + C) * NB + b
+            const int b = o % NB, C = (o / NB) % WSZ, R = o / (NB * WSZ);
+            float s = 0.f;
+            for (int jj = 0; jj < nlanes; jj++) {
+                const int cj = cis[w][jj];
+                if (cj == C) s += red[w][0][R][b][jj];
+                if (cj + 1 == C) s += red[w][1][R][b][jj];
+            }
+            v[h] = s;
+        }
+        wave_sync();
+        // ---- normalize (surfd.cu:2447-2493): sequential-addressing tree
+        float a = v[0] * v[0];
+        if (NF > 64) a = a + v[NF > 64 ? 1 : 0] * v[NF > 64 ? 1 : 0];
+#pragma unroll
+        for (int k = 32; k >= 1; k >>= 1) a = a + __shfl_down(a, k, 64);
+        const float fac = 1.f / sqrtf(__shfl(a, 0, 64));
+        float* out = desc + ((size_t)f * max_pts + kp) * NF;
+        out[lane] = v[0] * fac;
+        if (NF > 64) out[lane + 64] = v[NF > 64 ? 1 : 0] * fac;
+    }
+}
+
 hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
                            const int* counts, const int* offsets, int nframes, float* desc, hipStream_t s)
 {
     if (P.nfeat > 128) return hipErrorInvalidValue;
     const int grid = 2048;
-    if (P.upright) k_describe<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, counts, offsets, nframes, desc);
-    else k_describe<false><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, counts, offsets, nframes, desc);
+    if (P.upright && P.wsz == 4) {
+        if (P.extend) k_describe_ur<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, nframes, desc);
+        else k_describe_ur<false><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, nframes, desc);
+    } else if (P.upright) {
+        k_describe<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, counts, offsets, nframes, desc);
+    } else {
+        k_describe<false><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, counts, offsets, nframes, desc);
+    }
     return hipGetLastError();
 }
 
