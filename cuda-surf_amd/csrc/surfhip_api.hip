@@ -60,6 +60,9 @@ struct surfhip_detector {
     uint32_t* keys = nullptr;
     uint64_t* gscratch = nullptr;
     int* cand_count = nullptr;
+    uint32_t* scan_key = nullptr;       // NMS survivors awaiting interpolation
+    uint32_t* scan_src = nullptr;
+    int* scan_count = nullptr;
     int* offsets = nullptr;
     int* status = nullptr;
     // single-frame API slots
@@ -368,6 +371,7 @@ static int derive(surfhip_detector* d)
 static void free_all(surfhip_detector* d)
 {
     void* ptrs[] = {d->d_oct, d->ii, d->resp, d->colsum, d->cand, d->keys, d->gscratch, d->cand_count,
+                    d->scan_key, d->scan_src, d->scan_count,
                     d->offsets, d->status, d->pts1, d->desc1, d->count1};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -417,6 +421,9 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     ALLOC(d->cand, B * d->cap * sizeof(surfhip_point));
     ALLOC(d->keys, B * d->cap * sizeof(uint32_t));
     ALLOC(d->cand_count, B * sizeof(int));
+    ALLOC(d->scan_key, B * d->cap * sizeof(uint32_t));
+    ALLOC(d->scan_src, B * d->cap * sizeof(uint32_t));
+    ALLOC(d->scan_count, B * sizeof(int));
     ALLOC(d->offsets, (B + 1) * sizeof(int));
     ALLOC(d->status, 16);
     ALLOC(d->pts1, (size_t)max_pts * sizeof(surfhip_point));
@@ -505,13 +512,14 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
     hipStream_t s = d->stream;
     const bool prof = d->profiling;
     HIPCHK(hipMemsetAsync(d->cand_count, 0, sizeof(int) * nframes, s));
+    HIPCHK(hipMemsetAsync(d->scan_count, 0, sizeof(int) * nframes, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[0], s));
     HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[1], s));
     HIPCHK(launch_hessian(d->ii, d->resp, nframes, d->P, d->d_oct, d->oct[0], d->plan, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[2], s));
-    HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->cand, d->keys, d->cand_count,
-                      d->cap, s));
+    HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->scan_key, d->scan_src, d->scan_count,
+                      d->cap, d->cand, d->keys, d->cand_count, d->cap, d->status, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[3], s));
     HIPCHK(launch_sort(d->cand, d->keys, d->gscratch, d->cand_count, d->cap, nframes, points, d->max_pts,
                        counts, d->offsets, d->status, s));

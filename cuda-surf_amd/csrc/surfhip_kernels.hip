@@ -394,7 +394,7 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan)
             plan.hess_nbx[o] = (q.sw + 63) / 64;
             if (!(o == 0 && plan.o0_lds)) hb += plan.hess_nbx[o] * ((q.sh + 3) / 4);
             plan.nms_nbx[o] = (q.nms_gx + 63) / 64;
-            plan.nms_nby[o] = (q.nms_gy + 3) / 4;
+            plan.nms_nby[o] = (q.nms_gy + kScanRows - 1) / kScanRows;
             nb += 2 * plan.nms_nbx[o] * plan.nms_nby[o];
         } else {
             plan.hess_nbx[o] = plan.nms_nbx[o] = plan.nms_nby[o] = 1;
@@ -492,15 +492,15 @@ __device__ void solve3(float* sol, float (&sq)[3][3])
 // halfImage copies: planes 0/1 of octave o > 0 are read in place from octave
 // o-1's planes 2/4 at (2r, 2c), which is exactly what halfImage copied.
 struct OctView {
-    const float* cur;
-    const float* prev;
+    const float* F;                 // the frame's response block
+    int cur, prev;                  // float offsets of this octave's / the previous octave's plane 0 (-1: none)
     int sp, osize, psp, posize;
-    __device__ __forceinline__ float operator()(int s, int r, int c) const
+    __device__ __forceinline__ int off(int s, int r, int c) const
     {
-        if (prev != nullptr && s < 2)
-            return prev[(size_t)(s == 0 ? 2 : 4) * posize + (size_t)(2 * r) * psp + 2 * c];
-        return cur[(size_t)s * osize + (size_t)r * sp + c];
+        if (prev >= 0 && s < 2) return prev + (s == 0 ? 2 : 4) * posize + (2 * r) * psp + 2 * c;
+        return cur + s * osize + r * sp + c;
     }
+    __device__ __forceinline__ float operator()(int s, int r, int c) const { return F[off(s, r, c)]; }
 };
 
 __device__ float fit_quad(const OctView& V, float (&off)[3], int s, int r, int c)
@@ -556,8 +556,10 @@ __device__ __forceinline__ int32_t trace_sign(const uint32_t* __restrict__ I, in
     return ((int32_t)((uint32_t)lxx + (uint32_t)lyy) > 0) ? 1 : -1;
 }
 
-__device__ bool nms_point(const uint32_t* __restrict__ I, const OctView& V, const FrameParams& P,
-                          const OctaveParams& q, int o, int z, int x, int y, surfhip_point& pt)
+// 3x3x3 scale-space maximum test of one 2x2x2 block (surfd.cu:678-792):
+// on success returns the block's argmax (s, r, c).
+__device__ __forceinline__ bool nms_scan_block(const OctView& V, const FrameParams& P, const OctaveParams& q, int z,
+                                               int x, int y, int& s_out, int& r_out, int& c_out)
 {
     const int sw = q.sw, sh = q.sh;
     const int k = 2 * z + 1;
@@ -602,7 +604,18 @@ __device__ bool nms_point(const uint32_t* __restrict__ I, const OctView& V, cons
     if (best < V(s, r, cn) || best < V(s, rp, cn)) return false;
     if (best < V(si, rn, c - 1) || best < V(si, rn, c) || best < V(si, rn, c + 1)) return false;
     if (best < V(si, rp, cn) || best < V(si, r, cn)) return false;
+    s_out = s;
+    r_out = r;
+    c_out = c;
+    return true;
+}
 
+// Sub-pixel interpolation + acceptance + makePoint (surfd.cu:794-831,
+// 942-1022) for one NMS survivor.
+__device__ bool nms_fit_point(const uint32_t* __restrict__ I, const OctView& V, const FrameParams& P,
+                              const OctaveParams& q, int o, int s, int r, int c, surfhip_point& pt)
+{
+    const int sw = q.sw, sh = q.sh;
     float off[3] = {0.f, 0.f, 0.f};
     float strength = 0.f;
     int newr = r, newc = c;
@@ -652,12 +665,43 @@ __device__ bool nms_point(const uint32_t* __restrict__ I, const OctView& V, cons
     return true;
 }
 
-// All octaves and both NMS levels in one launch (blockIdx.x), frame = blockIdx.y.
-__global__ __launch_bounds__(256) void k_nms(const int32_t* __restrict__ ii, const float* __restrict__ resp,
-                                             FrameParams P, const OctaveParams* __restrict__ oct,
-                                             LaunchPlan plan, surfhip_point* __restrict__ cand,
-                                             uint32_t* __restrict__ keys, int* __restrict__ cand_count, int cap)
+__device__ __forceinline__ OctView make_view(const float* F, const OctaveParams& q, int o)
 {
+    OctView V;
+    V.F = F;
+    V.cur = (int)q.ooff;
+    V.prev = o > 0 ? (int)q.pooff : -1;
+    V.sp = q.sp;
+    V.osize = q.osize;
+    V.psp = q.psp;
+    V.posize = q.posize;
+    return V;
+}
+
+// Wave-aggregated append: one atomic per wave for all its `ok` lanes.
+__device__ __forceinline__ int wave_append(bool ok, int* counter)
+{
+    const unsigned long long m = __ballot(ok);
+    if (m == 0ull) return -1;
+    const int leader = __builtin_ctzll(m);
+    int base = 0;
+    if ((int)lane_id() == leader) base = atomicAdd(counter, (int)__popcll(m));
+    base = __shfl(base, leader, 64);
+    return ok ? base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))
+              : -1;
+}
+
+// Pass 1: the 3x3x3 test for every 2x2x2 block of every octave and both NMS
+// levels (blockIdx.x), frame = blockIdx.y.  Streams the response planes once;
+// survivors (~1 % of blocks) are appended to the frame's scan list with their
+// canonical key (octave, level, block row, block col) and argmax (s, r, c).
+__global__ __launch_bounds__(256) void k_nms_scan(const float* __restrict__ resp, FrameParams P,
+                                                  const OctaveParams* __restrict__ oct, LaunchPlan plan,
+                                                  uint32_t* __restrict__ scan_key, uint32_t* __restrict__ scan_src,
+                                                  int* __restrict__ scan_count, int scap)
+{
+    constexpr int NU = kScanRows / 4;        // block rows per thread
     const int o = octave_of(plan.nms_start, P.noct, blockIdx.x);
     const OctaveParams& q = oct[o];
     const int nbx = plan.nms_nbx[o], nby = plan.nms_nby[o];
@@ -665,45 +709,127 @@ __global__ __launch_bounds__(256) void k_nms(const int32_t* __restrict__ ii, con
     const int z = lb / (nbx * nby);
     lb -= z * nbx * nby;
     const int x = (lb % nbx) * 64 + (threadIdx.x & 63);
-    const int y = (lb / nbx) * 4 + (threadIdx.x >> 6);
+    const int y0 = (lb / nbx) * kScanRows + (threadIdx.x >> 6);
     const int f = blockIdx.y;
-    const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
-    const float* F = resp + (size_t)f * P.resp_stride;
-    OctView V;
-    V.cur = F + q.ooff;
-    V.prev = o > 0 ? F + q.pooff : nullptr;
-    V.sp = q.sp;
-    V.osize = q.osize;
-    V.psp = q.psp;
-    V.posize = q.posize;
+    const OctView V = make_view(resp + (size_t)f * P.resp_stride, q, o);
+    const int k = 2 * z + 1, mb = q.mb[z];
+    const int j = mb + x * 2;
+    // ---- issue every row's 2x2x2 block loads first (memory-level parallelism)
+    float v[NU][8];
+    bool in[NU];
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+        const int y = y0 + 4 * u, i = mb + y * 2;
+        in[u] = x < q.nms_gx && y < q.nms_gy && i < q.sh - mb && j < q.sw - mb;
+        const int ii = in[u] ? i : mb, jj = in[u] ? j : mb;
+        v[u][0] = V(k, ii, jj);
+        v[u][1] = V(k, ii, jj + 1);
+        v[u][2] = V(k, ii + 1, jj);
+        v[u][3] = V(k, ii + 1, jj + 1);
+        v[u][4] = V(k + 1, ii, jj);
+        v[u][5] = V(k + 1, ii, jj + 1);
+        v[u][6] = V(k + 1, ii + 1, jj);
+        v[u][7] = V(k + 1, ii + 1, jj + 1);
+    }
+    // ---- argmax + threshold, then the 19 outer neighbours for the rare survivors
+    bool ok[NU];
+    int ss[NU], rr[NU], cc[NU];
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+        int cas = 0;
+        float best = v[u][0];
+#pragma unroll
+        for (int t = 1; t < 8; t++)
+            if (v[u][t] > best) { best = v[u][t]; cas = t; }
+        const int i = mb + (y0 + 4 * u) * 2;
+        ok[u] = in[u] && !(best < P.thresh * 0.8f || (k + 1 == P.max_scale - 1 && cas > 3));
+        int s = k + (cas >> 2), r = i + ((cas >> 1) & 1), c = j + (cas & 1);
+        ss[u] = s; rr[u] = r; cc[u] = c;
+        if (ok[u]) {
+            const int ds = (cas >> 2) ? 1 : -1, dr = ((cas >> 1) & 1) ? 1 : -1, dc = (cas & 1) ? 1 : -1;
+            const int so = s + ds, si = s - ds;
+            const int rn = r + dr, rp = r - dr, cn = c + dc;
+            ok[u] = !(best < V(so, rp, c - 1) || best < V(so, rp, c) || best < V(so, rp, c + 1) ||
+                      best < V(so, r, c - 1) || best < V(so, r, c) || best < V(so, r, c + 1) ||
+                      best < V(so, rn, c - 1) || best < V(so, rn, c) || best < V(so, rn, c + 1) ||
+                      best < V(s, rn, c - 1) || best < V(s, rn, c) || best < V(s, rn, c + 1) ||
+                      best < V(s, r, cn) || best < V(s, rp, cn) ||
+                      best < V(si, rn, c - 1) || best < V(si, rn, c) || best < V(si, rn, c + 1) ||
+                      best < V(si, rp, cn) || best < V(si, r, cn));
+        }
+    }
+    // ---- one atomic per wave for all its survivors
+    unsigned long long m[NU];
+    int tot = 0;
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+        m[u] = __ballot(ok[u]);
+        tot += (int)__popcll(m[u]);
+    }
+    if (tot == 0) return;
+    const int leader = 0;
+    int base = 0;
+    if (lane_id() == (unsigned)leader) base = atomicAdd(&scan_count[f], tot);
+    base = __shfl(base, leader, 64);
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+        if (ok[u]) {
+            const int slot = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m[u] >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((unsigned)m[u], 0u));
+            if (slot < scap) {
+                const int y = y0 + 4 * u;
+                scan_key[(size_t)f * scap + slot] = ((uint32_t)o << 29) | ((uint32_t)z << 28) | ((uint32_t)y << 14) | (uint32_t)x;
+                scan_src[(size_t)f * scap + slot] = ((uint32_t)ss[u] << 28) | ((uint32_t)rr[u] << 14) | (uint32_t)cc[u];
+            }
+        }
+        base += (int)__popcll(m[u]);
+    }
+}
+
+// Pass 2: interpolation + makePoint, one lane per survivor (no divergence
+// against the ~99 % of blocks that fail the 3x3x3 test).
+__global__ __launch_bounds__(256) void k_nms_fit(const int32_t* __restrict__ ii, const float* __restrict__ resp,
+                                                 FrameParams P, const OctaveParams* __restrict__ oct,
+                                                 const uint32_t* __restrict__ scan_key,
+                                                 const uint32_t* __restrict__ scan_src,
+                                                 const int* __restrict__ scan_count, int scap,
+                                                 surfhip_point* __restrict__ cand, uint32_t* __restrict__ keys,
+                                                 int* __restrict__ cand_count, int cap, int* status)
+{
+    const int f = blockIdx.y;
+    const int n = scan_count[f];
+    if (blockIdx.x == 0 && threadIdx.x == 0 && n > scap) atomicOr(status, 4);
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (blockIdx.x * 256 >= min(n, scap)) return;            // whole block idle
     surfhip_point pt;
     bool ok = false;
-    if (x < q.nms_gx && y < q.nms_gy) ok = nms_point(I, V, P, q, o, z, x, y, pt);
-    const unsigned long long m = __ballot(ok);
-    if (m == 0ull) return;
-    const int leader = __builtin_ctzll(m);
-    const unsigned lane = lane_id();
-    int base = 0;
-    if ((int)lane == leader) base = atomicAdd(&cand_count[f], (int)__popcll(m));
-    base = __shfl(base, leader, 64);
-    if (ok) {
-        const int slot = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-        if (slot < cap) {
-            cand[(size_t)f * cap + slot] = pt;
-            keys[(size_t)f * cap + slot] = ((uint32_t)o << 29) | ((uint32_t)z << 28) |
-                                           ((uint32_t)y << 14) | (uint32_t)x;
-        }
+    uint32_t key = 0;
+    if (t < min(n, scap)) {
+        key = scan_key[(size_t)f * scap + t];
+        const uint32_t src = scan_src[(size_t)f * scap + t];
+        const int o = (int)(key >> 29);
+        const OctaveParams& q = oct[o];
+        const OctView V = make_view(resp + (size_t)f * P.resp_stride, q, o);
+        const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
+        ok = nms_fit_point(I, V, P, q, o, (int)(src >> 28), (int)((src >> 14) & 0x3fffu), (int)(src & 0x3fffu), pt);
+    }
+    const int slot = wave_append(ok, &cand_count[f]);
+    if (slot >= 0 && slot < cap) {
+        cand[(size_t)f * cap + slot] = pt;
+        keys[(size_t)f * cap + slot] = key;
     }
 }
 
 hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,
-                      const OctaveParams* d_oct, const LaunchPlan& plan, surfhip_point* cand,
-                      uint32_t* keys, int* cand_count, int cap, hipStream_t s)
+                      const OctaveParams* d_oct, const LaunchPlan& plan, uint32_t* scan_key, uint32_t* scan_src,
+                      int* scan_count, int scap, surfhip_point* cand, uint32_t* keys, int* cand_count, int cap,
+                      int* status, hipStream_t s)
 {
     if (plan.nms_start[kMaxOct] == 0) return hipSuccess;
-    dim3 grid(plan.nms_start[kMaxOct], nframes);
-    k_nms<<<grid, 256, 0, s>>>(ii, resp, P, d_oct, plan, cand, keys, cand_count, cap);
+    k_nms_scan<<<dim3(plan.nms_start[kMaxOct], nframes), 256, 0, s>>>(resp, P, d_oct, plan, scan_key, scan_src,
+                                                                      scan_count, scap);
+    k_nms_fit<<<dim3((scap + 255) / 256, nframes), 256, 0, s>>>(ii, resp, P, d_oct, scan_key, scan_src, scan_count,
+                                                                 scap, cand, keys, cand_count, cap, status);
     return hipGetLastError();
 }
 
@@ -1165,7 +1291,10 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
     constexpr int WSZ = 4;
     constexpr int NB = EXT ? 8 : 4;                       // bins per cell
     constexpr int NF = WSZ * WSZ * NB;
-    __shared__ float red[4][2][WSZ][NB][64];              // [wave][k][R][bin][lane]
+    // [wave][k][lane][R * NB + bin], rows padded to an odd stride: the
+    // per-lane writes and the per-output reads are both conflict-free
+    constexpr int RS = WSZ * NB + 1;
+    __shared__ float red[4][2][64][RS];
     __shared__ int cis[4][64];
     const unsigned lane = lane_id();
     const int w = threadIdx.x >> 6;
@@ -1208,6 +1337,7 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
 #pragma unroll
                 for (int b = 0; b < NB; b++) acc[k][R][b] = 0.f;
         for (int si = -iradius; si <= iradius; si++) {
+          {
             const float rpos = ((float)(step * si) - dy0) / spacing;
             const float rx = rpos + wofs;
             const int r = iy + si * step;
@@ -1248,6 +1378,7 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
                     acc[1][R][2 * t + 1] += odd ? v1 : 0.f;
                 }
             }
+          }
         }
         // ---- ordered cross-lane reduction into the 16 cells
 #pragma unroll
@@ -1255,7 +1386,7 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
 #pragma unroll
             for (int R = 0; R < WSZ; R++)
 #pragma unroll
-                for (int b = 0; b < NB; b++) red[w][k][R][b][lane] = acc[k][R][b];
+                for (int b = 0; b < NB; b++) red[w][k][lane][R * NB + b] = acc[k][R][b];
         cis[w][lane] = col_on ? ci : -100;
         wave_sync();
         const int nlanes = min(2 * iradius + 1, 64);
@@ -1267,8 +1398,8 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
             float s = 0.f;
             for (int jj = 0; jj < nlanes; jj++) {
                 const int cj = cis[w][jj];
-                if (cj == C) s += red[w][0][R][b][jj];
-                if (cj + 1 == C) s += red[w][1][R][b][jj];
+                if (cj == C) s += red[w][0][jj][R * NB + b];
+                if (cj + 1 == C) s += red[w][1][jj][R * NB + b];
             }
             v[h] = s;
         }
