@@ -253,22 +253,28 @@ __device__ __forceinline__ float hessian_at(const uint32_t* __restrict__ I, int 
 }
 
 // ----------------------------------------------------------------------
-// Octave 0 (sampling 2 => 2 px between samples, lobes 3..11): LDS tiles.
+// Octave 0 (sampling 2 => 2 px between samples, lobes 3..11): LDS ring.
 // 85 % of all responses live here and every integral value is re-read ~40
-// times, so a workgroup stages a tile of the integral image in LDS with
-// coalesced 16-B loads and computes 128 x 16 samples x 5 scales from it.
-// Layout: parity planes (even / odd image columns) of *pairs*
-//   T[row][p][k] = (I[row][xs + 2k + p], I[row][xs + 2k + p + 128])
+// times.  A workgroup owns a vertical strip of 128 sample columns of one
+// frame and walks it top to bottom, streaming the integral rows through an
+// LDS ring of 64 rows: each image row of the strip is read from HBM once
+// (column halo 1.125x), and the loads of the next 16 rows are in flight while
+// the 8 waves compute the current 8 sample rows.
+// Row layout: parity planes (even / odd image columns) of *pairs*
+//   T[slot][p][k] = (I[row][xs + 2k + p], I[row][xs + 2k + p + 128])
 // so lane l, which owns samples ix and ix + 64 (x0 and x0 + 128 px), gets
-// both samples' corner with ONE conflict-free ds_read_b64 whose offset is a
-// compile-time immediate (the lobe geometry is fixed for init_lobe 3).
-// 64 rows x 2 planes x 80 pairs x 8 B = 80 KiB -> two workgroups per CU.
+// both samples' corner with ONE conflict-free ds_read_b64 whose column offset
+// is a compile-time immediate (the lobe geometry is fixed for init_lobe 3);
+// the ring slot of a corner row is wave-uniform (scalar ALU).
+// 64 slots x 2 planes x 80 pairs x 8 B = 80 KiB -> two workgroups per CU.
 // ----------------------------------------------------------------------
 namespace o0 {
-constexpr int TXS = 128;                 // samples per tile row (64 lanes x 2)
-constexpr int TYS = 16;                  // sample rows per tile
-constexpr int NR = 2 * TYS + 32;         // image rows: y0 - 16 .. y0 + 17 over the tile
+constexpr int TXS = 128;                 // sample columns per strip (64 lanes x 2)
 constexpr int NK = 80;                   // pairs per parity-plane row
+constexpr int ROWQ = 2 * NK;             // uint64 per ring slot
+constexpr int NRING = 64;                // ring slots (image rows)
+constexpr int STEP = 16;                 // image rows per step = 8 sample rows
+constexpr int ITEMS = STEP * 40;         // fill items per step: (row, 4-column group)
 constexpr int THREADS = 512;
 }
 
@@ -278,10 +284,11 @@ constexpr int THREADS = 512;
 typedef const volatile uint64_t __attribute__((address_space(3))) lds_u64;
 
 template <int M, int X2, int X3, int X4>
-__device__ __forceinline__ void hess_pair(const lds_u64* Tb, float norm, float& ha, float& hb)
+__device__ __forceinline__ void hess_pair(const lds_u64* Tl, int sb, float norm, float& ha, float& hb)
 {
-    // corner (dr, dc) relative to (y0, x0); Tb points at row y0 - 16, lane l
-#define C(dr, dc) Tb[((dr) + 16) * 2 * o0::NK + ((dc) & 1) * o0::NK + ((16 + (dc)) >> 1)]
+    // corner (dr, dc) relative to (y0, x0); slot sb holds image row y0 - 16,
+    // Tl points at pair `lane` of slot 0
+#define C(dr, dc) Tl[((sb + 16 + (dr)) & (o0::NRING - 1)) * o0::ROWQ + ((dc) & 1) * o0::NK + ((16 + (dc)) >> 1)]
     const uint64_t a1 = C(X3 + 1, M + X2 + 1), a2 = C(-X3, -M - X2), a3 = C(-X3, M + X2 + 1), a4 = C(X3 + 1, -M - X2);
     const uint64_t b1 = C(X3 + 1, X2 + 1), b2 = C(-X3, -X2), b3 = C(-X3, X2 + 1), b4 = C(X3 + 1, -X2);
     const uint64_t c1 = C(M + X2 + 1, X3 + 1), c2 = C(-M - X2, -X3), c3 = C(-M - X2, X3 + 1), c4 = C(M + X2 + 1, -X3);
@@ -315,11 +322,11 @@ __device__ __forceinline__ void hess_pair(const lds_u64* Tb, float norm, float& 
 }
 
 template <int S, int M, int X2, int X3, int X4>
-__device__ __forceinline__ void hess_store(const lds_u64* Tb, const OctaveParams& q, float* row, int iy,
+__device__ __forceinline__ void hess_store(const lds_u64* Tl, int sb, const OctaveParams& q, float* row, int iy,
                                            int ixa, int ixb)
 {
     float ha, hb;
-    hess_pair<M, X2, X3, X4>(Tb, q.norm[S], ha, hb);
+    hess_pair<M, X2, X3, X4>(Tl, sb, q.norm[S], ha, hb);
     const int b1 = q.b1[S];
     const bool vy = iy >= b1 && iy < q.sh - b1;
     float* pl = row + (size_t)S * q.osize;
@@ -327,43 +334,97 @@ __device__ __forceinline__ void hess_store(const lds_u64* Tb, const OctaveParams
     if (ixb < q.sw) pl[ixb] = (vy && ixb >= b1 && ixb < q.sw - b1) ? hb : 0.f;
 }
 
-__global__ __launch_bounds__(o0::THREADS, 4) void k_hess_o0(const int32_t* __restrict__ ii, float* __restrict__ resp,
-                                                            FrameParams P, OctaveParams q, int nbx)
+// One fill item: image row gy, columns xs + 4a .. + 3 and the same + 128.
+struct RowItem { uint4 g0, g1; };
+
+__device__ __forceinline__ RowItem o0_load(const uint32_t* __restrict__ I, const FrameParams& P, int gy, int gx)
 {
-    __shared__ __attribute__((aligned(16))) uint64_t T[o0::NR * 2 * o0::NK];
-    const int bx = blockIdx.x % nbx, by = blockIdx.x / nbx, f = blockIdx.y;
-    const int IX0 = bx * o0::TXS, IY0 = by * o0::TYS;
-    const int xs = 2 * IX0 - 16, ys = 2 * IY0 - 16;
+    RowItem v;
+    v.g0 = make_uint4(0u, 0u, 0u, 0u);
+    v.g1 = v.g0;
+    if (gy >= 0 && gy < P.iH) {
+        const uint32_t* row = I + (size_t)gy * P.ip;
+        if (gx >= 0 && gx < P.ip) v.g0 = *reinterpret_cast<const uint4*>(row + gx);
+        if (gx + 128 < P.ip) v.g1 = *reinterpret_cast<const uint4*>(row + gx + 128);
+    }
+    return v;
+}
+
+__device__ __forceinline__ void o0_store(uint64_t* T, int gy, int a, const RowItem& v)
+{
+    uint64_t* dst = T + (gy & (o0::NRING - 1)) * o0::ROWQ + 2 * a;
+    *reinterpret_cast<uint4*>(dst) = make_uint4(v.g0.x, v.g1.x, v.g0.z, v.g1.z);            // even plane
+    *reinterpret_cast<uint4*>(dst + o0::NK) = make_uint4(v.g0.y, v.g1.y, v.g0.w, v.g1.w);   // odd plane
+}
+
+__global__ __launch_bounds__(o0::THREADS, 4) void k_hess_o0(const int32_t* __restrict__ ii, float* __restrict__ resp,
+                                                            FrameParams P, OctaveParams q, int nstrips, int nframes)
+{
+    __shared__ __attribute__((aligned(16))) uint64_t T[o0::NRING * o0::ROWQ];
+    // XCD-aware order: the workgroups of XCD x (blockIdx % 8) take frames
+    // x, x + 8, ..., all strips of a frame together, so the strips' shared
+    // halo columns are served from that XCD's L2.
+    const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
+    const int f = (k / nstrips) * 8 + xcd, bx = k % nstrips;
+    if (f >= nframes) return;
+    const int IX0 = bx * o0::TXS;
+    const int xs = 2 * IX0 - 16;
     const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
-    // ---- fill: item (row, a) loads image columns xs+4a.. and xs+4a+128..
-    for (int t = threadIdx.x; t < o0::NR * 40; t += o0::THREADS) {
-        const int ry = t / 40, a = t - ry * 40;
-        const int gy = ys + ry, gx = xs + 4 * a;
-        uint4 g0 = make_uint4(0u, 0u, 0u, 0u), g1 = g0;
-        if (gy >= 0 && gy < P.iH) {
-            const uint32_t* row = I + (size_t)gy * P.ip;
-            if (gx >= 0 && gx < P.ip) g0 = *reinterpret_cast<const uint4*>(row + gx);
-            if (gx + 128 < P.ip) g1 = *reinterpret_cast<const uint4*>(row + gx + 128);
-        }
-        uint64_t* dst = T + ry * 2 * o0::NK + 2 * a;
-        *reinterpret_cast<uint4*>(dst) = make_uint4(g0.x, g1.x, g0.z, g1.z);            // even plane, k = 2a, 2a+1
-        *reinterpret_cast<uint4*>(dst + o0::NK) = make_uint4(g0.y, g1.y, g0.w, g1.w);   // odd plane
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // item it of a 16-row chunk starting at image row y: row y + it / 40, group it % 40
+    const int ra0 = tid / 40, ga0 = tid - ra0 * 40;                 // it = tid          (< 640)
+    const int it1 = tid + o0::THREADS;                               // it = tid + 512    (< 640 for tid < 128)
+    const int ra1 = it1 / 40, ga1 = it1 - ra1 * 40;
+    const bool has1 = it1 < o0::ITEMS;
+    // ---- prologue: image rows -16 .. 31
+    for (int y = -16; y < 32; y += o0::STEP) {
+        const RowItem v0 = o0_load(I, P, y + ra0, xs + 4 * ga0);
+        RowItem v1;
+        if (has1) v1 = o0_load(I, P, y + ra1, xs + 4 * ga1);
+        o0_store(T, y + ra0, ga0, v0);
+        if (has1) o0_store(T, y + ra1, ga1, v1);
     }
     __syncthreads();
-    // ---- compute: wave w owns sample rows w, w + 8; lane l samples ix, ix + 64
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const lds_u64* Tl = (const lds_u64*)T + lane;
     const int ixa = IX0 + lane, ixb = ixa + 64;
     float* F = resp + (size_t)f * P.resp_stride + q.ooff;
-    for (int r = w; r < o0::TYS; r += o0::THREADS / 64) {
-        const int iy = IY0 + r;
-        if (iy >= q.sh) break;
-        const lds_u64* Tb = (const lds_u64*)(T + (2 * r) * 2 * o0::NK + lane);    // image row y0 - 16
-        float* row = F + (size_t)iy * q.sp;
-        hess_store<0, 3, 1, 2, 3>(Tb, q, row, iy, ixa, ixb);
-        hess_store<1, 5, 2, 4, 6>(Tb, q, row, iy, ixa, ixb);
-        hess_store<2, 7, 3, 6, 9>(Tb, q, row, iy, ixa, ixb);
-        hess_store<3, 9, 4, 8, 12>(Tb, q, row, iy, ixa, ixb);
-        hess_store<4, 11, 5, 10, 15>(Tb, q, row, iy, ixa, ixb);
+    const int nsteps = (q.sh + 7) >> 3;
+    // Two-deep prefetch: the rows step s + 2 adds (16 s + 48 ..) are loaded
+    // at the start of step s and written to the ring at the end of step s + 1,
+    // so each load has two steps of compute to land.  The rows step s + 1
+    // adds (16 s + 32 ..) go into the slots of rows 16 s - 32 .., last read
+    // in step s - 1.
+    RowItem pa0, pa1, pb0, pb1;
+    pa0 = o0_load(I, P, 32 + ra0, xs + 4 * ga0);
+    if (has1) pa1 = o0_load(I, P, 32 + ra1, xs + 4 * ga1);
+    auto step = [&](int s, RowItem& cur0, RowItem& cur1, RowItem& nxt0, RowItem& nxt1) {
+        const int yl = 16 * s + 48;                 // rows loaded now, for step s + 2
+        if (s + 2 < nsteps) {
+            nxt0 = o0_load(I, P, yl + ra0, xs + 4 * ga0);
+            if (has1) nxt1 = o0_load(I, P, yl + ra1, xs + 4 * ga1);
+        }
+        const int iy = 8 * s + w;
+        if (iy < q.sh) {
+            const int sb = (2 * iy - 16) & (o0::NRING - 1);
+            float* row = F + (size_t)iy * q.sp;
+            hess_store<0, 3, 1, 2, 3>(Tl, sb, q, row, iy, ixa, ixb);
+            hess_store<1, 5, 2, 4, 6>(Tl, sb, q, row, iy, ixa, ixb);
+            hess_store<2, 7, 3, 6, 9>(Tl, sb, q, row, iy, ixa, ixb);
+            hess_store<3, 9, 4, 8, 12>(Tl, sb, q, row, iy, ixa, ixb);
+            hess_store<4, 11, 5, 10, 15>(Tl, sb, q, row, iy, ixa, ixb);
+        }
+        if (s + 1 < nsteps) {
+            const int yw = 16 * s + 32;             // rows step s + 1 needs
+            o0_store(T, yw + ra0, ga0, cur0);
+            if (has1) o0_store(T, yw + ra1, ga1, cur1);
+        }
+        __syncthreads();
+    };
+    for (int s = 0; s < nsteps; s += 2) {
+        step(s, pa0, pa1, pb0, pb1);
+        if (s + 1 < nsteps) step(s + 1, pb0, pb1, pa0, pa1);
     }
 }
 
@@ -384,8 +445,8 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan)
 {
     int hb = 0, nb = 0;
     plan.o0_lds = P.noct > 0 && o0_lds_ok(P, oct[0]);
-    plan.o0_nbx = (oct[0].sw + o0::TXS - 1) / o0::TXS;
-    plan.o0_blocks = plan.o0_nbx * ((oct[0].sh + o0::TYS - 1) / o0::TYS);
+    plan.o0_nbx = (oct[0].sw + o0::TXS - 1) / o0::TXS;     // strips per frame
+    plan.o0_blocks = plan.o0_nbx;
     for (int o = 0; o < kMaxOct; o++) {
         plan.hess_start[o] = hb;
         plan.nms_start[o] = nb;
@@ -445,7 +506,8 @@ hipError_t launch_hessian(const int32_t* ii, float* resp, int nframes, const Fra
                           hipStream_t s)
 {
     if (plan.o0_lds)
-        k_hess_o0<<<dim3(plan.o0_blocks, nframes), o0::THREADS, 0, s>>>(ii, resp, P, q0, plan.o0_nbx);
+        k_hess_o0<<<dim3(((nframes + 7) & ~7) * plan.o0_nbx), o0::THREADS, 0, s>>>(ii, resp, P, q0, plan.o0_nbx,
+                                                                                   nframes);
     if (plan.hess_start[kMaxOct] > 0)
         k_hessian<<<dim3(plan.hess_start[kMaxOct], nframes), 256, 0, s>>>(ii, resp, P, d_oct, plan);
     return hipGetLastError();
@@ -1271,17 +1333,40 @@ __global__ __launch_bounds__(256) void k_describe(const int32_t* __restrict__ ii
 
 // ----------------------------------------------------------------------
 // Upright descriptor (U-SURF, 4x4 cells), deterministic and atomic-free.
-// The upright sample grid is separable: a sample's cell row (ri, rfrac)
-// depends only on its grid row i and its cell column (ci, cfrac) only on its
-// grid column j (surfd.cu:1290-1294).  So lane = grid column j, the wave
-// walks the rows i (cell row wave-uniform), and each lane accumulates its
-// placeInIndex contributions (surfd.cu:1199-1271) for cell columns ci and
-// ci+1 in registers.  A fixed-order cross-lane reduction through LDS then
-// forms the 16 cells.  Per-sample weights are the reference's exact float
-// products; only the summation order differs from the oracle's (<= 1e-6).
-// iradius <= 22 for wsz 4 (7.5 * scale / step, step = rn(scale / 2)), so the
-// (2 iradius + 1) columns fit one wave.
+// The upright sample grid is separable (surfd.cu:1290-1294): a sample's cell
+// row (ri, rfrac) depends only on its grid row i, its cell column (ci, cfrac)
+// only on its grid column j.  So:
+//  * lane = grid column j; when the grid is at most 32 columns wide (iradius
+//    <= 15, ~2/3 of keypoints) the two half-waves walk alternate grid rows,
+//    so no lane idles on the wide-grid padding;
+//  * the rows are walked in cell-row bands (ri = -1..3, contiguous because ri
+//    is monotonic in i), each band compile-time, so the placeInIndex row
+//    weights (1 - rfrac, rfrac) go into fixed registers: per band a lane keeps
+//    P = sum v and Q = sum v * rfrac, then row ri gets P - Q and row ri + 1
+//    gets Q (surfd.cu:1199-1271 with the sums regrouped);
+//  * bins are kept as (total, negative part) pairs, so the sign-selected
+//    bins cost a min/select instead of a branch;
+//  * the column weights (1 - cfrac, cfrac) are applied once per lane in a
+//    fixed-order reduction over the lanes of each cell column.
+// Grid-row geometry (rpos, rx, ri, rfrac) is computed once per row, with the
+// reference's exact float operations, so cell membership and the lookup2
+// index match the oracle bit for bit; only the summation order differs
+// (<= 1e-6 relative, inside the 1e-4 descriptor tolerance).
+// Integral-image reads are raw buffer loads (SGPR descriptor + 32-bit
+// offsets, no 64-bit address arithmetic).  iradius <= 22 for wsz 4, so the
+// grid fits one wave.
 // ----------------------------------------------------------------------
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const uint32_t* I, long long nbytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc((void*)I, (short)0, (int)nbytes, 0x00020000);
+}
+__device__ __forceinline__ uint32_t bld(__amdgpu_buffer_rsrc_t r, int off)
+{
+    return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
+
+template <int R> struct IntC { static constexpr int value = R; };
+
 template <bool EXT>
 __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__ ii, FrameParams P,
                                                      const surfhip_point* __restrict__ pts, int max_pts,
@@ -1291,26 +1376,53 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
     constexpr int WSZ = 4;
     constexpr int NB = EXT ? 8 : 4;                       // bins per cell
     constexpr int NF = WSZ * WSZ * NB;
-    // [wave][k][lane][R * NB + bin], rows padded to an odd stride: the
-    // per-lane writes and the per-output reads are both conflict-free
-    constexpr int RS = WSZ * NB + 1;
-    __shared__ float red[4][2][64][RS];
-    __shared__ int cis[4][64];
-    const unsigned lane = lane_id();
-    const int w = threadIdx.x >> 6;
+    constexpr int RS = WSZ * NB + 1;                      // odd stride: conflict-free writes
+    __shared__ float red[4][64][RS];
+    __shared__ float s_cf[4][64];
+    __shared__ float s_rf[4][64], s_rp[4][64];
+    __shared__ unsigned long long s_mask[4][6];
+    __shared__ float s_lut[40];
+    if (threadIdx.x < 40) s_lut[threadIdx.x] = c_tab.lut2[threadIdx.x];
+    __syncthreads();
+    const int lane = (int)lane_id();
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);     // wave-uniform: SGPR descriptors
     const int total = offsets[nframes];
     const float fw = (float)WSZ;
     const float wofs = (float)WSZ * 0.5f - 0.5f;
-    for (int g = blockIdx.x * 4 + w; g < total; g += gridDim.x * 4) {
+    // XCD-aware split: the workgroups of one XCD (blockIdx % 8) take one
+    // contiguous eighth of the keypoints, i.e. a few whole frames, so the
+    // integral-image patches they gather stay in that XCD's L2.
+    const int xcd = blockIdx.x & 7, nbx = gridDim.x >> 3, lb = blockIdx.x >> 3;
+    const int chunk = (total + 7) >> 3;
+    const int gbeg = xcd * chunk, gend = min(total, gbeg + chunk);
+    // the wave's keypoints ascend, so its frame is tracked incrementally
+    // (one binary search per wave) and the next keypoint is fetched while
+    // the current one is described
+    const int gstride = nbx * 4;
+    int gn = gbeg + lb * 4 + w;
+    int fn = 0, fnb = 0, fne = 0;
+    surfhip_point pn;
+    if (gn < gend) {
         int lo = 0, hi = nframes;
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
-            if (offsets[mid] <= g) lo = mid; else hi = mid;
+            if (offsets[mid] <= gn) lo = mid; else hi = mid;
         }
-        const int f = lo, kp = g - offsets[lo];
-        const surfhip_point p = pts[(size_t)f * max_pts + kp];
+        fn = lo;
+        fnb = offsets[lo];
+        fne = offsets[lo + 1];
+        pn = pts[(size_t)fn * max_pts + (gn - fnb)];
+    }
+    while (gn < gend) {
+        const int f = fn, kp = gn - fnb;
+        const surfhip_point p = pn;
+        gn += gstride;
+        if (gn < gend) {
+            while (gn >= fne) { fn++; fnb = fne; fne = offsets[fn + 1]; }
+            pn = pts[(size_t)fn * max_pts + (gn - fnb)];
+        }
         const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
-        const int ip = P.ip;
+        const __amdgpu_buffer_rsrc_t rsrc = frame_rsrc(I, P.ii_stride * 4);
         const float scale = 1.65f * p.scale;
         const int step = max(f2i_rn(scale * 0.5f), 1);
         const int ix = f2i_rn(p.x), iy = f2i_rn(p.y);
@@ -1319,100 +1431,141 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
         const int hs = f2i_rz(scale);
         const int rlim = P.iH - 1 - hs, clim = P.W - hs;
         const int iradius = f2i_rn(((spacing * (float)(WSZ + 1)) * 0.5f) / (float)step);
-        // ---- per-lane column geometry
-        const int sj = (int)lane - iradius;
+        const int side = 2 * iradius + 1;
+        const bool dual = side <= 32;
+        // ---- grid row t = lane: exact row geometry (surfd.cu:1290-1292)
+        const int sit = lane - iradius;
+        const float rpos_t = ((float)(step * sit) - dy0) / spacing;
+        const float rx_t = rpos_t + wofs;
+        const int r_t = iy + sit * step;
+        const bool rvalid = lane < side && rx_t > -1.f && rx_t < fw && r_t >= 1 + hs && r_t < rlim;
+        const int ri_t = f2i_rz(rx_t >= 0.f ? rx_t : rx_t - 1.f);
+        s_rf[w][lane] = rx_t - (float)ri_t;
+        s_rp[w][lane] = rpos_t * rpos_t;
+        // ---- grid column of this lane
+        const int j = dual ? (lane & 31) : lane;
+        const int h = dual ? (lane >> 5) : 0;
+        const int rstep = dual ? 2 : 1;
+        const int sj = j - iradius;
         const float cpos = ((float)(step * sj) - dx0) / spacing;
         const float cx = cpos + wofs;
         const int c = ix + sj * step;
-        const bool col_on = (int)lane <= 2 * iradius && cx > -1.f && cx < fw && c >= 1 + hs && c < clim;
+        const bool col_on = j < side && cx > -1.f && cx < fw && c >= 1 + hs && c < clim;
         const int ci = f2i_rz(cx >= 0.f ? cx : cx - 1.f);
         const float cfrac = cx - (float)ci;
-        const float cfrac1 = 1 - cfrac;
-        const bool k0 = col_on && ci >= 0, k1 = col_on && ci + 1 < WSZ;
-        float acc[2][WSZ][NB];
+        const float cp2 = cpos * cpos;
+        const int ip4 = P.ip * 4;
+        const int oA = (c - hs) * 4, oB = (c + hs + 1) * 4, oC = c * 4;
+        const int dR0 = -hs * ip4, dR3 = (hs + 1) * ip4;
+        wave_sync();
+        constexpr int NS = EXT ? 8 : 4;
+        float acc[WSZ][NS];
 #pragma unroll
-        for (int k = 0; k < 2; k++)
+        for (int R = 0; R < WSZ; R++)
 #pragma unroll
-            for (int R = 0; R < WSZ; R++)
+            for (int s = 0; s < NS; s++) acc[R][s] = 0.f;
+        auto band = [&](auto Rc) {
+            constexpr int R = decltype(Rc)::value;
+            const unsigned long long m = __ballot(rvalid && ri_t == R);
+            if (m == 0ull) return;
+            const int r0 = __builtin_ctzll(m), n = __builtin_popcountll(m);
+            float Ps[NS], Qs[NS];
 #pragma unroll
-                for (int b = 0; b < NB; b++) acc[k][R][b] = 0.f;
-        for (int si = -iradius; si <= iradius; si++) {
-          {
-            const float rpos = ((float)(step * si) - dy0) / spacing;
-            const float rx = rpos + wofs;
-            const int r = iy + si * step;
-            if (!(rx > -1.f && rx < fw && r >= 1 + hs && r < rlim)) continue;     // wave-uniform
-            const int ri = f2i_rz(rx >= 0.f ? rx : rx - 1.f);
-            const float rfrac = rx - (float)ri;
-            if (!col_on) continue;
-            const float weight = c_tab.lut2[f2i_rz(rpos * rpos + cpos * cpos)];
-            const float dx = (weight * (float)wavelet2(I, ip, c, r, hs)) * INV255;
-            const float dy = (weight * (float)wavelet1(I, ip, c, r, hs)) * INV255;
-            // the (mag, bin) pairs placeInIndex receives (surfd.cu:1306-1314)
-            float mag[4];
-            int bin[4];
-            if constexpr (!EXT) {
-                mag[0] = dx; bin[0] = dx < 0 ? 0 : 1;
-                mag[1] = dy; bin[1] = dy < 0 ? 2 : 3;
-            } else {
-                mag[0] = dx; bin[0] = dy < 0 ? 0 : 1;
-                mag[1] = fabsf(dx); bin[1] = dy < 0 ? 2 : 3;
-                mag[2] = dy; bin[2] = dx < 0 ? 4 : 5;
-                mag[3] = fabsf(dy); bin[3] = dx < 0 ? 6 : 7;
-            }
-            constexpr int NM = EXT ? 4 : 2;
+            for (int s = 0; s < NS; s++) Ps[s] = Qs[s] = 0.f;
+            if (col_on) {
+                for (int k = h; k < n; k += rstep) {
+                    const int tt = r0 + k;
+                    const float rf = s_rf[w][tt];
+                    const float rp = s_rp[w][tt];
+                    const int rb = (iy + (tt - iradius) * step) * ip4;
+                    const int q0 = rb + dR0, q2 = rb + ip4, q3 = rb + dR3;
+                    // corners (row, col): rows r-s, r, r+1, r+s+1; cols c-s, c+s+1, c, c+1
+                    const uint32_t a00 = bld(rsrc, q0 + oA), a01 = bld(rsrc, q0 + oB);
+                    const uint32_t a02 = bld(rsrc, q0 + oC), a03 = bld(rsrc, q0 + oC + 4);
+                    const uint32_t a10 = bld(rsrc, rb + oA), a11 = bld(rsrc, rb + oB);
+                    const uint32_t a20 = bld(rsrc, q2 + oA), a21 = bld(rsrc, q2 + oB);
+                    const uint32_t a30 = bld(rsrc, q3 + oA), a31 = bld(rsrc, q3 + oB);
+                    const uint32_t a32 = bld(rsrc, q3 + oC), a33 = bld(rsrc, q3 + oC + 4);
+                    // haarX / haarY (surfd.cu:1171-1182 via getSum)
+                    const int32_t wav1 = (int32_t)((a21 + a00 - a01 - a20) - (a31 + a10 - a11 - a30));
+                    const int32_t wav2 = (int32_t)((a31 + a02 - a01 - a32) - (a33 + a00 - a03 - a30));
+                    const float weight = s_lut[f2i_rz(rp + cp2)];
+                    const float dx = (weight * (float)wav2) * INV255;
+                    const float dy = (weight * (float)wav1) * INV255;
+                    float S[NS];
+                    if constexpr (!EXT) {
+                        S[0] = dx; S[1] = fminf(dx, 0.f);          // bins 1 | 0 by sign of dx
+                        S[2] = dy; S[3] = fminf(dy, 0.f);          // bins 3 | 2 by sign of dy
+                    } else {
+                        const float adx = fabsf(dx), ady = fabsf(dy);
+                        S[0] = dx;  S[1] = dy < 0.f ? dx : 0.f;    // bins 1 | 0 by sign of dy
+                        S[2] = adx; S[3] = dy < 0.f ? adx : 0.f;   // bins 3 | 2
+                        S[4] = dy;  S[5] = dx < 0.f ? dy : 0.f;    // bins 5 | 4 by sign of dx
+                        S[6] = ady; S[7] = dx < 0.f ? ady : 0.f;   // bins 7 | 6
+                    }
 #pragma unroll
-            for (int R = 0; R < WSZ; R++) {
-                if (R != ri && R != ri + 1) continue;                             // wave-uniform
-                const float rw = (R == ri) ? (1.f - rfrac) : rfrac;
-#pragma unroll
-                for (int t = 0; t < NM; t++) {
-                    const float rv = mag[t] * rw;
-                    const float v0 = k0 ? rv * cfrac1 : 0.f;
-                    const float v1 = k1 ? rv * cfrac : 0.f;
-                    // mag t always lands in bin 2t or 2t + 1
-                    const bool odd = bin[t] & 1;
-                    acc[0][R][2 * t] += odd ? 0.f : v0;
-                    acc[0][R][2 * t + 1] += odd ? v0 : 0.f;
-                    acc[1][R][2 * t] += odd ? 0.f : v1;
-                    acc[1][R][2 * t + 1] += odd ? v1 : 0.f;
+                    for (int s = 0; s < NS; s++) {
+                        Ps[s] += S[s];
+                        Qs[s] = fmaf(S[s], rf, Qs[s]);
+                    }
                 }
             }
-          }
-        }
-        // ---- ordered cross-lane reduction into the 16 cells
 #pragma unroll
-        for (int k = 0; k < 2; k++)
-#pragma unroll
-            for (int R = 0; R < WSZ; R++)
-#pragma unroll
-                for (int b = 0; b < NB; b++) red[w][k][lane][R * NB + b] = acc[k][R][b];
-        cis[w][lane] = col_on ? ci : -100;
-        wave_sync();
-        const int nlanes = min(2 * iradius + 1, 64);
-        float v[2];
-#pragma unroll
-        for (int h = 0; h < (NF + 63) / 64; h++) {
-            const int o = (int)lane + 64 * h;            // output index (R * WSZ + C) * NB + b
-            const int b = o % NB, C = (o / NB) % WSZ, R = o / (NB * WSZ);
-            float s = 0.f;
-            for (int jj = 0; jj < nlanes; jj++) {
-                const int cj = cis[w][jj];
-                if (cj == C) s += red[w][0][jj][R * NB + b];
-                if (cj + 1 == C) s += red[w][1][jj][R * NB + b];
+            for (int s = 0; s < NS; s++) {
+                if constexpr (R >= 0) acc[R][s] += Ps[s] - Qs[s];
+                if constexpr (R + 1 < WSZ) acc[R + 1][s] += Qs[s];
             }
-            v[h] = s;
+        };
+        band(IntC<-1>{});
+        band(IntC<0>{});
+        band(IntC<1>{});
+        band(IntC<2>{});
+        band(IntC<3>{});
+        // ---- per-lane bins, then the fixed-order column reduction
+#pragma unroll
+        for (int R = 0; R < WSZ; R++)
+#pragma unroll
+            for (int q = 0; q < NB / 2; q++) {
+                red[w][lane][R * NB + 2 * q] = acc[R][2 * q + 1];                    // negative part
+                red[w][lane][R * NB + 2 * q + 1] = acc[R][2 * q] - acc[R][2 * q + 1];
+            }
+        s_cf[w][lane] = cfrac;
+#pragma unroll
+        for (int C = -1; C < WSZ; C++) {
+            const unsigned long long mc = __ballot(col_on && ci == C);
+            if (lane == 0) s_mask[w][C + 1] = mc;
+        }
+        wave_sync();
+        float v[NF / 64];
+#pragma unroll
+        for (int hh = 0; hh < NF / 64; hh++) {
+            const int o = lane + 64 * hh;                 // (R * WSZ + C) * NB + b
+            const int b = o % NB, C = (o / NB) % WSZ, R = o / (NB * WSZ);
+            const int col = R * NB + b;
+            unsigned long long m0 = s_mask[w][C + 1], m1 = s_mask[w][C];
+            float s = 0.f;
+            while (m0) {
+                const int jj = __builtin_ctzll(m0);
+                m0 &= m0 - 1;
+                s += red[w][jj][col] * (1.f - s_cf[w][jj]);
+            }
+            while (m1) {
+                const int jj = __builtin_ctzll(m1);
+                m1 &= m1 - 1;
+                s += red[w][jj][col] * s_cf[w][jj];
+            }
+            v[hh] = s;
         }
         wave_sync();
         // ---- normalize (surfd.cu:2447-2493): sequential-addressing tree
         float a = v[0] * v[0];
-        if (NF > 64) a = a + v[NF > 64 ? 1 : 0] * v[NF > 64 ? 1 : 0];
+        if constexpr (NF > 64) a = a + v[NF / 64 - 1] * v[NF / 64 - 1];
 #pragma unroll
         for (int k = 32; k >= 1; k >>= 1) a = a + __shfl_down(a, k, 64);
         const float fac = 1.f / sqrtf(__shfl(a, 0, 64));
         float* out = desc + ((size_t)f * max_pts + kp) * NF;
         out[lane] = v[0] * fac;
-        if (NF > 64) out[lane + 64] = v[NF > 64 ? 1 : 0] * fac;
+        if constexpr (NF > 64) out[lane + 64] = v[NF / 64 - 1] * fac;
     }
 }
 
