@@ -499,7 +499,7 @@ int surfhip_run_integral(surfhip_detector* d, const uint8_t* frames, int nframes
 int surfhip_run_hessian(surfhip_detector* d, int nframes)
 {
     if (!d || nframes < 1 || nframes > d->max_batch) return SURFHIP_ERR_INVALID;
-    HIPCHK(launch_hessian(d->ii, d->resp, nframes, d->P, d->d_oct, d->oct[0], d->plan, d->stream));
+    HIPCHK(launch_hessian(d->ii, d->resp, nframes, d->P, d->d_oct, d->oct, d->plan, d->stream));
     return SURFHIP_OK;
 }
 
@@ -516,7 +516,7 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
     if (prof) HIPCHK(hipEventRecord(d->ev[0], s));
     HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[1], s));
-    HIPCHK(launch_hessian(d->ii, d->resp, nframes, d->P, d->d_oct, d->oct[0], d->plan, s));
+    HIPCHK(launch_hessian(d->ii, d->resp, nframes, d->P, d->d_oct, d->oct, d->plan, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[2], s));
     HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->scan_key, d->scan_src, d->scan_count,
                       d->cap, d->cand, d->keys, d->cand_count, d->cap, d->status, s));

@@ -66,11 +66,13 @@ struct LaunchPlan {
     int nms_nbx[kMaxOct], nms_nby[kMaxOct];
     int o0_lds;                     // octave 0 on the LDS-tiled kernel (k_hess_o0)
     int o0_nbx, o0_blocks;
+    int o1_lds;                     // octave 1 on the LDS ring (k_hess_o1)
+    int o1_nbx;
 };
 void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan);
 
 hipError_t launch_hessian(const int32_t* ii, float* resp, int nframes, const FrameParams& P,
-                          const OctaveParams* d_oct, const OctaveParams& q0, const LaunchPlan& plan,
+                          const OctaveParams* d_oct, const OctaveParams* h_oct, const LaunchPlan& plan,
                           hipStream_t s);
 hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,
                       const OctaveParams* d_oct, const LaunchPlan& plan, uint32_t* scan_key, uint32_t* scan_src,

@@ -192,6 +192,90 @@ __global__ __launch_bounds__(256) void k_ii_fill(const uint8_t* __restrict__ fra
     }
 }
 
+// Pass (C) with one wave per band and no barriers: lane l owns columns
+// 4 l + 256 t + j (t < NT, j < 4), so every load is 256 contiguous bytes and
+// every store 1 KiB; the row scan is NT wave scans with a running carry.
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total)
+{
+    const unsigned lane = lane_id();
+    uint32_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t n = (uint32_t)__shfl_up((int)inc, d, 64);
+        if (lane >= (unsigned)d) inc += n;
+    }
+    total = (uint32_t)__shfl((int)inc, 63, 64);
+    return inc - v;
+}
+
+template <int NT>
+__global__ __launch_bounds__(256) void k_ii_fill_w(const uint8_t* __restrict__ frames, int pitch,
+                                                   long long fstride, int W, int H, int nbands,
+                                                   const uint32_t* __restrict__ colpre, int CW,
+                                                   int32_t* __restrict__ ii, int ip, long long istride, int nframes)
+{
+    const int gw = blockIdx.x * 4 + (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int f = gw / nbands, band = gw - f * nbands;
+    if (f >= nframes) return;
+    const int lane = (int)lane_id();
+    const int y0 = band * kBandRows;
+    const int rows = min(kBandRows, H - y0);
+    // acc = ii[y0][x]: exclusive row scan of the column sums above the band
+    uint32_t acc[NT][4];
+    {
+        const uint32_t* c = colpre + ((size_t)f * nbands + band) * CW;
+        uint32_t carry = 0u;
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+            const int x = 4 * lane + 256 * t;
+            uint32_t v[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) v[j] = (x + j < W) ? c[x + j] : 0u;
+            const uint32_t e1 = v[0], e2 = e1 + v[1], e3 = e2 + v[2], tot = e3 + v[3];
+            uint32_t wt;
+            const uint32_t base = carry + wave_excl_scan(tot, wt);
+            carry += wt;
+            acc[t][0] = base; acc[t][1] = base + e1; acc[t][2] = base + e2; acc[t][3] = base + e3;
+        }
+    }
+    uint32_t* out = reinterpret_cast<uint32_t*>(ii) + (size_t)f * istride;
+    if (band == 0) {
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+            const int x = 4 * lane + 256 * t;
+            if (x < ip) *reinterpret_cast<uint4*>(out + x) = make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
+    const uint8_t* src = frames + (size_t)f * fstride + (size_t)y0 * pitch;
+    for (int r = 0; r < rows; r++) {
+        const uint8_t* row = src + (size_t)r * pitch;
+        uint32_t wv[NT];
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+            const int x = 4 * lane + 256 * t;
+            wv[t] = (x + 4 <= pitch) ? *reinterpret_cast<const uint32_t*>(row + x) : 0u;
+        }
+        uint32_t* dst = out + (size_t)(y0 + r + 1) * ip;
+        uint32_t carry = 0u;
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+            const int x = 4 * lane + 256 * t;
+            uint32_t p[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) p[j] = (x + j < W) ? (wv[t] >> (8 * j)) & 0xffu : 0u;
+            const uint32_t e1 = p[0], e2 = e1 + p[1], e3 = e2 + p[2], tot = e3 + p[3];
+            uint32_t wt;
+            const uint32_t base = carry + wave_excl_scan(tot, wt);
+            carry += wt;
+            acc[t][0] += base; acc[t][1] += base + e1; acc[t][2] += base + e2; acc[t][3] += base + e3;
+            // pad columns (> W) stay zero: the flat reads of getTrace can land on them
+            if (x < ip)
+                *reinterpret_cast<uint4*>(dst + x) = make_uint4(x <= W ? acc[t][0] : 0u, x + 1 <= W ? acc[t][1] : 0u,
+                                                                x + 2 <= W ? acc[t][2] : 0u, x + 3 <= W ? acc[t][3] : 0u);
+        }
+    }
+}
+
 hipError_t launch_integral(const uint8_t* frames, int pitch, long long fstride, int nframes,
                            const FrameParams& P, uint32_t* colsum, int32_t* ii, hipStream_t s)
 {
@@ -202,12 +286,14 @@ hipError_t launch_integral(const uint8_t* frames, int pitch, long long fstride, 
         const int CW = 2048;
         k_ii_bandsum<8><<<grid, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW);
         k_ii_bandscan<<<dim3((W + 255) / 256, nframes), 256, 0, s>>>(colsum, nbands, CW, W);
-        k_ii_fill<8><<<grid, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW, ii, P.ip, P.ii_stride);
+        k_ii_fill_w<8><<<(nbands * nframes + 3) / 4, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW,
+                                                                    ii, P.ip, P.ii_stride, nframes);
     } else if (W + 1 <= 4096) {
         const int CW = 4096;
         k_ii_bandsum<16><<<grid, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW);
         k_ii_bandscan<<<dim3((W + 255) / 256, nframes), 256, 0, s>>>(colsum, nbands, CW, W);
-        k_ii_fill<16><<<grid, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW, ii, P.ip, P.ii_stride);
+        k_ii_fill_w<16><<<(nbands * nframes + 3) / 4, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum,
+                                                                     CW, ii, P.ip, P.ii_stride, nframes);
     } else {
         return hipErrorInvalidValue;
     }
@@ -428,6 +514,154 @@ __global__ __launch_bounds__(o0::THREADS, 4) void k_hess_o0(const int32_t* __res
     }
 }
 
+// ----------------------------------------------------------------------
+// Octave 1 (4 px between samples, lobes 15/19/23: corner offsets -34..35):
+// the same strip walk with an LDS ring, one workgroup per CU.  A strip is
+// 64 sample columns (lane = sample); each ring slot holds image columns
+// xs .. xs + 323 (xs = 4 * IX0 - 36) split into 4 residue planes
+//   T[slot][c & 3][c >> 2]   (c = column - xs)
+// so the 64 lanes' reads of one corner are 64 consecutive dwords.  A step is
+// 4 sample rows (16 image rows); its window is rows y - 34 .. y + 47, and the
+// ring of 98 slots leaves room for the 16 rows of the next step.  12 waves:
+// wave (r, scale) computes one sample row of one scale per step.
+// ----------------------------------------------------------------------
+namespace o1 {
+constexpr int TXS = 64;                  // sample columns per strip
+constexpr int NK = 81;                   // dwords per residue plane
+constexpr int ROWD = 4 * NK;             // dwords per ring slot
+constexpr int NRING = 98;                // ring slots (image rows)
+constexpr int LO = 34;                   // rows above a sample row in its window
+constexpr int STEP = 16;                 // image rows per step = 4 sample rows
+constexpr int ITEMS = STEP * NK;         // fill items per step: (row, 4-column group)
+constexpr int THREADS = 768;
+}
+
+template <int M, int X2, int X3, int X4>
+__device__ __forceinline__ float hess1(const uint32_t* Tl, int sb, float norm)
+{
+    // corner (dr, dc) relative to (y0, x0); slot sb holds image row y0 - 34
+#define SLOT(dr) ((sb + LOFF + (dr)) >= o1::NRING ? (sb + LOFF + (dr)) - o1::NRING : (sb + LOFF + (dr)))
+#define C(dr, dc) Tl[SLOT(dr) * o1::ROWD + ((dc) & 3) * o1::NK + ((36 + (dc)) >> 2)]
+    constexpr int LOFF = o1::LO;
+    const uint32_t a1 = C(X3 + 1, M + X2 + 1), a2 = C(-X3, -M - X2), a3 = C(-X3, M + X2 + 1), a4 = C(X3 + 1, -M - X2);
+    const uint32_t b1 = C(X3 + 1, X2 + 1), b2 = C(-X3, -X2), b3 = C(-X3, X2 + 1), b4 = C(X3 + 1, -X2);
+    const uint32_t c1 = C(M + X2 + 1, X3 + 1), c2 = C(-M - X2, -X3), c3 = C(-M - X2, X3 + 1), c4 = C(M + X2 + 1, -X3);
+    const uint32_t d1 = C(X2 + 1, X3 + 1), d2 = C(-X2, -X3), d3 = C(-X2, X3 + 1), d4 = C(X2 + 1, -X3);
+    const uint32_t s1a = C(1, X4 + 1), s1b = C(-X4, 0), s1c = C(-X4, X4 + 1), s1d = C(1, 0);
+    const uint32_t s2a = C(X4 + 1, 1), s2b = C(0, -X4), s2c = C(0, 1), s2d = C(X4 + 1, -X4);
+    const uint32_t s3a = C(X4 + 1, X4 + 1), s3b = C(0, 0), s3c = C(0, X4 + 1), s3d = C(X4 + 1, 0);
+    const uint32_t s4a = C(1, 1), s4b = C(-X4, -X4), s4c = C(-X4, 1), s4d = C(1, -X4);
+#undef C
+#undef SLOT
+    const uint32_t A = a1 + a2 - a3 - a4, B = b1 + b2 - b3 - b4;
+    const uint32_t Cc = c1 + c2 - c3 - c4, D = d1 + d2 - d3 - d4;
+    const uint32_t S1 = s1a + s1b - s1c - s1d, S2 = s2a + s2b - s2c - s2d;
+    const uint32_t S3 = s3a + s3b - s3c - s3d, S4 = s4a + s4b - s4c - s4d;
+    const float rr = INV255 * INV255;
+    const float dxx = (float)(int32_t)(A - 3u * B);
+    const float dyy = (float)(int32_t)(Cc - 3u * D);
+    const float dxy = 0.6f * (float)(int32_t)(S1 + S2 - S3 - S4);
+    const float p = dxx * dyy;
+    const float q2 = dxy * dxy;
+    return (rr * (p - q2)) * norm;
+}
+
+__device__ __forceinline__ uint4 o1_load(const uint32_t* __restrict__ I, const FrameParams& P, int gy, int gx)
+{
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (gy >= 0 && gy < P.iH && gx >= 0 && gx < P.ip)
+        v = *reinterpret_cast<const uint4*>(I + (size_t)gy * P.ip + gx);
+    return v;
+}
+
+__device__ __forceinline__ void o1_store(uint32_t* T, int gy, int a, uint4 v)
+{
+    const int slot = (gy + 2 * o1::NRING) % o1::NRING;
+    uint32_t* dst = T + slot * o1::ROWD + a;
+    dst[0] = v.x;
+    dst[o1::NK] = v.y;
+    dst[2 * o1::NK] = v.z;
+    dst[3 * o1::NK] = v.w;
+}
+
+__global__ __launch_bounds__(o1::THREADS, 1) void k_hess_o1(const int32_t* __restrict__ ii, float* __restrict__ resp,
+                                                            FrameParams P, OctaveParams q, int nstrips, int nframes)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t T[o1::NRING * o1::ROWD];
+    const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
+    const int f = (k / nstrips) * 8 + xcd, bx = k % nstrips;
+    if (f >= nframes) return;
+    const int IX0 = bx * o1::TXS;
+    const int xs = 4 * IX0 - 36;
+    const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ra0 = tid / o1::NK, ga0 = tid - ra0 * o1::NK;                 // item tid
+    const int it1 = tid + o1::THREADS;                                      // item tid + 768
+    const int ra1 = it1 / o1::NK, ga1 = it1 - ra1 * o1::NK;
+    const bool has1 = it1 < o1::ITEMS;
+    // ---- prologue: image rows -34 .. 47 (step 0's window)
+    for (int it = tid; it < 82 * o1::NK; it += o1::THREADS) {
+        const int r = it / o1::NK, a = it - r * o1::NK;
+        o1_store(T, r - 34, a, o1_load(I, P, r - 34, xs + 4 * a));
+    }
+    __syncthreads();
+    const uint32_t* Tl = T + lane;
+    const int ix = IX0 + lane;
+    float* F = resp + (size_t)f * P.resp_stride + q.ooff;
+    const int nsteps = (q.sh + 3) >> 2;
+    const int ur = w & 3, us = w >> 2;            // this wave's (sample row, scale) unit
+    const int b1 = q.b1[us];
+    const float norm = q.norm[us];
+    float* plane = F + (size_t)(q.init_scale + us) * q.osize;
+    // two-deep prefetch, as in k_hess_o0: rows 16 s + 64 .. (step s + 2) load
+    // now and land in the ring at the end of step s + 1
+    uint4 pa0 = make_uint4(0u, 0u, 0u, 0u), pa1 = pa0, pb0 = pa0, pb1 = pa0;
+    pa0 = o1_load(I, P, 48 + ra0, xs + 4 * ga0);
+    if (has1) pa1 = o1_load(I, P, 48 + ra1, xs + 4 * ga1);
+    auto step = [&](int s, uint4& cur0, uint4& cur1, uint4& nxt0, uint4& nxt1) {
+        const int yl = 16 * s + 64;
+        if (s + 2 < nsteps) {
+            nxt0 = o1_load(I, P, yl + ra0, xs + 4 * ga0);
+            if (has1) nxt1 = o1_load(I, P, yl + ra1, xs + 4 * ga1);
+        }
+        const int iy = 4 * s + ur;
+        if (iy < q.sh) {
+            const int sb = (4 * iy - 34 + 2 * o1::NRING) % o1::NRING;
+            float h;
+            if (us == 0) h = hess1<15, 7, 14, 21>(Tl, sb, norm);
+            else if (us == 1) h = hess1<19, 9, 18, 27>(Tl, sb, norm);
+            else h = hess1<23, 11, 22, 33>(Tl, sb, norm);
+            const bool v = iy >= b1 && iy < q.sh - b1 && ix >= b1 && ix < q.sw - b1;
+            if (ix < q.sw) plane[(size_t)iy * q.sp + ix] = v ? h : 0.f;
+        }
+        if (s + 1 < nsteps) {
+            const int yw = 16 * s + 48;
+            o1_store(T, yw + ra0, ga0, cur0);
+            if (has1) o1_store(T, yw + ra1, ga1, cur1);
+        }
+        __syncthreads();
+    };
+    for (int s = 0; s < nsteps; s += 2) {
+        step(s, pa0, pa1, pb0, pb1);
+        if (s + 1 < nsteps) step(s + 1, pb0, pb1, pa0, pa1);
+    }
+}
+
+// Octave 1 takes the LDS ring when its geometry is the one compiled into
+// k_hess_o1 (sampling 2, init lobe 3: lobes 15/19/23, planes 2..4).
+static bool o1_lds_ok(const FrameParams& P, const OctaveParams& q)
+{
+    static const int masks[3] = {15, 19, 23};
+    if (P.sampling != 2 || q.delta != 4 || q.nscale != 3 || q.init_scale != 2) return false;
+    for (int i = 0; i < 3; i++)
+        if (q.mask[i] != masks[i] || q.x2[i] != masks[i] / 2 || q.x3[i] != 2 * (masks[i] / 2) ||
+            q.x4[i] != 3 * (masks[i] / 2))
+            return false;
+    return true;
+}
+
 // Octave 0 takes the LDS path when its geometry is the fixed one compiled
 // into k_hess_o0 (sampling 2, lobes 3/5/7/9/11).
 static bool o0_lds_ok(const FrameParams& P, const OctaveParams& q)
@@ -447,13 +681,15 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan)
     plan.o0_lds = P.noct > 0 && o0_lds_ok(P, oct[0]);
     plan.o0_nbx = (oct[0].sw + o0::TXS - 1) / o0::TXS;     // strips per frame
     plan.o0_blocks = plan.o0_nbx;
+    plan.o1_lds = P.noct > 1 && o1_lds_ok(P, oct[1]);
+    plan.o1_nbx = P.noct > 1 ? (oct[1].sw + o1::TXS - 1) / o1::TXS : 0;
     for (int o = 0; o < kMaxOct; o++) {
         plan.hess_start[o] = hb;
         plan.nms_start[o] = nb;
         if (o < P.noct) {
             const OctaveParams& q = oct[o];
             plan.hess_nbx[o] = (q.sw + 63) / 64;
-            if (!(o == 0 && plan.o0_lds)) hb += plan.hess_nbx[o] * ((q.sh + 3) / 4);
+            if (!(o == 0 && plan.o0_lds) && !(o == 1 && plan.o1_lds)) hb += plan.hess_nbx[o] * ((q.sh + 3) / 4);
             plan.nms_nbx[o] = (q.nms_gx + 63) / 64;
             plan.nms_nby[o] = (q.nms_gy + kScanRows - 1) / kScanRows;
             nb += 2 * plan.nms_nbx[o] * plan.nms_nby[o];
@@ -472,19 +708,32 @@ __device__ __forceinline__ int octave_of(const int* start, int noct, int b)
     return o;
 }
 
-// All octaves of a frame in one launch: blockIdx.x walks the octaves' sample
-// grids (64 x 4 samples per block), blockIdx.y is the frame.
+// 1-D grid of nf8 * per workgroups, XCD-aware: the workgroups of XCD x
+// (blockIdx % 8) take frames x, x + 8, ..., each frame's `per` workgroups
+// together, so a frame's integral image / response planes are fetched into
+// one XCD's L2 instead of all eight.
+__device__ __forceinline__ bool xcd_frame_block(int per, int nframes, int& f, int& lb)
+{
+    const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
+    f = (k / per) * 8 + xcd;
+    lb = k - (k / per) * per;
+    return f < nframes;
+}
+
+// All octaves (not on an LDS ring) of a frame in one launch: the local block
+// index walks the octaves' sample grids (64 x 4 samples per block).
 __global__ __launch_bounds__(256) void k_hessian(const int32_t* __restrict__ ii, float* __restrict__ resp,
                                                  FrameParams P, const OctaveParams* __restrict__ oct,
-                                                 LaunchPlan plan)
+                                                 LaunchPlan plan, int nframes)
 {
-    const int o = octave_of(plan.hess_start, P.noct, blockIdx.x);
+    int f, gb;
+    if (!xcd_frame_block(plan.hess_start[kMaxOct], nframes, f, gb)) return;
+    const int o = octave_of(plan.hess_start, P.noct, gb);
     const OctaveParams& q = oct[o];
-    const int lb = blockIdx.x - plan.hess_start[o];
+    const int lb = gb - plan.hess_start[o];
     const int nbx = plan.hess_nbx[o];
     const int ix = (lb % nbx) * 64 + (threadIdx.x & 63);
     const int iy = (lb / nbx) * 4 + (threadIdx.x >> 6);
-    const int f = blockIdx.y;
     if (ix >= q.sw || iy >= q.sh) return;
     const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
     float* R = resp + (size_t)f * P.resp_stride + q.ooff + (size_t)iy * q.sp + ix;
@@ -502,14 +751,16 @@ __global__ __launch_bounds__(256) void k_hessian(const int32_t* __restrict__ ii,
 }
 
 hipError_t launch_hessian(const int32_t* ii, float* resp, int nframes, const FrameParams& P,
-                          const OctaveParams* d_oct, const OctaveParams& q0, const LaunchPlan& plan,
+                          const OctaveParams* d_oct, const OctaveParams* h_oct, const LaunchPlan& plan,
                           hipStream_t s)
 {
+    const int nf8 = (nframes + 7) & ~7;
     if (plan.o0_lds)
-        k_hess_o0<<<dim3(((nframes + 7) & ~7) * plan.o0_nbx), o0::THREADS, 0, s>>>(ii, resp, P, q0, plan.o0_nbx,
-                                                                                   nframes);
+        k_hess_o0<<<dim3(nf8 * plan.o0_nbx), o0::THREADS, 0, s>>>(ii, resp, P, h_oct[0], plan.o0_nbx, nframes);
+    if (plan.o1_lds)
+        k_hess_o1<<<dim3(nf8 * plan.o1_nbx), o1::THREADS, 0, s>>>(ii, resp, P, h_oct[1], plan.o1_nbx, nframes);
     if (plan.hess_start[kMaxOct] > 0)
-        k_hessian<<<dim3(plan.hess_start[kMaxOct], nframes), 256, 0, s>>>(ii, resp, P, d_oct, plan);
+        k_hessian<<<dim3(nf8 * plan.hess_start[kMaxOct]), 256, 0, s>>>(ii, resp, P, d_oct, plan, nframes);
     return hipGetLastError();
 }
 
@@ -761,18 +1012,19 @@ __device__ __forceinline__ int wave_append(bool ok, int* counter)
 __global__ __launch_bounds__(256) void k_nms_scan(const float* __restrict__ resp, FrameParams P,
                                                   const OctaveParams* __restrict__ oct, LaunchPlan plan,
                                                   uint32_t* __restrict__ scan_key, uint32_t* __restrict__ scan_src,
-                                                  int* __restrict__ scan_count, int scap)
+                                                  int* __restrict__ scan_count, int scap, int nframes)
 {
     constexpr int NU = kScanRows / 4;        // block rows per thread
-    const int o = octave_of(plan.nms_start, P.noct, blockIdx.x);
+    int f, gb;
+    if (!xcd_frame_block(plan.nms_start[kMaxOct], nframes, f, gb)) return;
+    const int o = octave_of(plan.nms_start, P.noct, gb);
     const OctaveParams& q = oct[o];
     const int nbx = plan.nms_nbx[o], nby = plan.nms_nby[o];
-    int lb = blockIdx.x - plan.nms_start[o];
+    int lb = gb - plan.nms_start[o];
     const int z = lb / (nbx * nby);
     lb -= z * nbx * nby;
     const int x = (lb % nbx) * 64 + (threadIdx.x & 63);
     const int y0 = (lb / nbx) * kScanRows + (threadIdx.x >> 6);
-    const int f = blockIdx.y;
     const OctView V = make_view(resp + (size_t)f * P.resp_stride, q, o);
     const int k = 2 * z + 1, mb = q.mb[z];
     const int j = mb + x * 2;
@@ -888,8 +1140,8 @@ hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const F
                       int* status, hipStream_t s)
 {
     if (plan.nms_start[kMaxOct] == 0) return hipSuccess;
-    k_nms_scan<<<dim3(plan.nms_start[kMaxOct], nframes), 256, 0, s>>>(resp, P, d_oct, plan, scan_key, scan_src,
-                                                                      scan_count, scap);
+    k_nms_scan<<<dim3(((nframes + 7) & ~7) * plan.nms_start[kMaxOct]), 256, 0, s>>>(resp, P, d_oct, plan, scan_key,
+                                                                                     scan_src, scan_count, scap, nframes);
     k_nms_fit<<<dim3((scap + 255) / 256, nframes), 256, 0, s>>>(ii, resp, P, d_oct, scan_key, scan_src, scan_count,
                                                                  scap, cand, keys, cand_count, cap, status);
     return hipGetLastError();
