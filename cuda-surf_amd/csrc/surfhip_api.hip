@@ -64,6 +64,7 @@ struct surfhip_detector {
     uint32_t* scan_src = nullptr;
     int* scan_count = nullptr;
     int* offsets = nullptr;
+    int* order = nullptr;               // per frame: keypoint indices in row order (describe schedule)
     int* status = nullptr;
     // single-frame API slots
     surfhip_point* pts1 = nullptr;
@@ -372,7 +373,7 @@ static void free_all(surfhip_detector* d)
 {
     void* ptrs[] = {d->d_oct, d->ii, d->resp, d->colsum, d->cand, d->keys, d->gscratch, d->cand_count,
                     d->scan_key, d->scan_src, d->scan_count,
-                    d->offsets, d->status, d->pts1, d->desc1, d->count1};
+                    d->offsets, d->order, d->status, d->pts1, d->desc1, d->count1};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (int i = 0; i < SURFHIP_NSTAGE; i++)
@@ -425,6 +426,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     ALLOC(d->scan_src, B * d->cap * sizeof(uint32_t));
     ALLOC(d->scan_count, B * sizeof(int));
     ALLOC(d->offsets, (B + 1) * sizeof(int));
+    ALLOC(d->order, B * (size_t)max_pts * sizeof(int));
     ALLOC(d->status, 16);
     ALLOC(d->pts1, (size_t)max_pts * sizeof(surfhip_point));
     ALLOC(d->desc1, (size_t)max_pts * d->param.nfeatures * sizeof(float));
@@ -519,13 +521,13 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
     HIPCHK(launch_hessian(d->ii, d->resp, nframes, d->P, d->d_oct, d->oct, d->plan, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[2], s));
     HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->scan_key, d->scan_src, d->scan_count,
-                      d->cap, d->cand, d->keys, d->cand_count, d->cap, d->status, s));
+                      d->cap, d->cand, d->keys, d->cand_count, d->cap, d->status, d->offsets, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[3], s));
     HIPCHK(launch_sort(d->cand, d->keys, d->gscratch, d->cand_count, d->cap, nframes, points, d->max_pts,
-                       counts, d->offsets, d->status, s));
+                       counts, d->offsets, d->order, d->status, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[4], s));
     if (desc)
-        HIPCHK(launch_describe(d->ii, d->P, points, d->max_pts, counts, d->offsets, nframes, desc, s));
+        HIPCHK(launch_describe(d->ii, d->P, points, d->max_pts, counts, d->offsets, d->order, nframes, desc, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[5], s));
     d->last_nframes = nframes;
     return SURFHIP_OK;

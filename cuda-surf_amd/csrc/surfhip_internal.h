@@ -77,12 +77,12 @@ hipError_t launch_hessian(const int32_t* ii, float* resp, int nframes, const Fra
 hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,
                       const OctaveParams* d_oct, const LaunchPlan& plan, uint32_t* scan_key, uint32_t* scan_src,
                       int* scan_count, int scap, surfhip_point* cand, uint32_t* keys, int* cand_count, int cap,
-                      int* status, hipStream_t s);
+                      int* status, int* scratch_off, hipStream_t s);
 hipError_t launch_sort(const surfhip_point* cand, const uint32_t* keys, uint64_t* gscratch,
                        int* cand_count, int cap, int nframes, surfhip_point* out, int max_pts,
-                       int* out_count, int* offsets, int* status, hipStream_t s);
+                       int* out_count, int* offsets, int* order, int* status, hipStream_t s);
 hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
-                           const int* counts, const int* offsets, int nframes, float* desc,
+                           const int* counts, const int* offsets, const int* order, int nframes, float* desc,
                            hipStream_t s);
 hipError_t launch_pack(const surfhip_point* pts, const float* desc, const int* counts, const int* offsets,
                        int nframes, int max_pts, int nfeat, uint8_t* slab, hipStream_t s);

@@ -814,6 +814,20 @@ struct OctView {
         return cur + s * osize + r * sp + c;
     }
     __device__ __forceinline__ float operator()(int s, int r, int c) const { return F[off(s, r, c)]; }
+    // (s, r, c) and (s, r, c + 1): one 8-byte load on a materialised plane
+    // (dword alignment is enough for global_load_dwordx2)
+    __device__ __forceinline__ void pair(int s, int r, int c, float& a, float& b) const
+    {
+        struct __attribute__((packed, aligned(4))) F2 { float x, y; };
+        if (prev >= 0 && s < 2) {
+            a = F[off(s, r, c)];
+            b = F[off(s, r, c + 1)];
+        } else {
+            const F2 v = *reinterpret_cast<const F2*>(F + off(s, r, c));
+            a = v.x;
+            b = v.y;
+        }
+    }
 };
 
 __device__ float fit_quad(const OctView& V, float (&off)[3], int s, int r, int c)
@@ -1006,25 +1020,25 @@ __device__ __forceinline__ int wave_append(bool ok, int* counter)
 }
 
 // Pass 1: the 3x3x3 test for every 2x2x2 block of every octave and both NMS
-// levels (blockIdx.x), frame = blockIdx.y.  Streams the response planes once;
-// survivors (~1 % of blocks) are appended to the frame's scan list with their
-// canonical key (octave, level, block row, block col) and argmax (s, r, c).
-__global__ __launch_bounds__(256) void k_nms_scan(const float* __restrict__ resp, FrameParams P,
-                                                  const OctaveParams* __restrict__ oct, LaunchPlan plan,
-                                                  uint32_t* __restrict__ scan_key, uint32_t* __restrict__ scan_src,
-                                                  int* __restrict__ scan_count, int scap, int nframes)
+// levels.  Streams the response planes once; survivors (~1 % of blocks) are
+// appended to the frame's scan list with their canonical key (octave, level,
+// block row, block col) and argmax (s, r, c).
+// One workgroup = 4 waves x (64 block columns x kScanRows/4 block rows) of
+// one (frame, octave, level); XCD x takes frames x, x + 8, ...
+__device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, const FrameParams& P,
+                                              const OctaveParams* __restrict__ oct, const LaunchPlan& plan,
+                                              uint32_t* __restrict__ scan_key, uint32_t* __restrict__ scan_src,
+                                              int* __restrict__ scan_count, int scap, int f, int gb, int wv)
 {
-    constexpr int NU = kScanRows / 4;        // block rows per thread
-    int f, gb;
-    if (!xcd_frame_block(plan.nms_start[kMaxOct], nframes, f, gb)) return;
+    constexpr int NU = kScanRows / 4;        // block rows per lane
     const int o = octave_of(plan.nms_start, P.noct, gb);
     const OctaveParams& q = oct[o];
     const int nbx = plan.nms_nbx[o], nby = plan.nms_nby[o];
     int lb = gb - plan.nms_start[o];
     const int z = lb / (nbx * nby);
     lb -= z * nbx * nby;
-    const int x = (lb % nbx) * 64 + (threadIdx.x & 63);
-    const int y0 = (lb / nbx) * kScanRows + (threadIdx.x >> 6);
+    const int x = (lb % nbx) * 64 + (int)lane_id();
+    const int y0 = (lb / nbx) * kScanRows + wv;
     const OctView V = make_view(resp + (size_t)f * P.resp_stride, q, o);
     const int k = 2 * z + 1, mb = q.mb[z];
     const int j = mb + x * 2;
@@ -1036,14 +1050,10 @@ __global__ __launch_bounds__(256) void k_nms_scan(const float* __restrict__ resp
         const int y = y0 + 4 * u, i = mb + y * 2;
         in[u] = x < q.nms_gx && y < q.nms_gy && i < q.sh - mb && j < q.sw - mb;
         const int ii = in[u] ? i : mb, jj = in[u] ? j : mb;
-        v[u][0] = V(k, ii, jj);
-        v[u][1] = V(k, ii, jj + 1);
-        v[u][2] = V(k, ii + 1, jj);
-        v[u][3] = V(k, ii + 1, jj + 1);
-        v[u][4] = V(k + 1, ii, jj);
-        v[u][5] = V(k + 1, ii, jj + 1);
-        v[u][6] = V(k + 1, ii + 1, jj);
-        v[u][7] = V(k + 1, ii + 1, jj + 1);
+        V.pair(k, ii, jj, v[u][0], v[u][1]);
+        V.pair(k, ii + 1, jj, v[u][2], v[u][3]);
+        V.pair(k + 1, ii, jj, v[u][4], v[u][5]);
+        V.pair(k + 1, ii + 1, jj, v[u][6], v[u][7]);
     }
     // ---- argmax + threshold, then the 19 outer neighbours for the rare survivors
     bool ok[NU];
@@ -1081,10 +1091,9 @@ __global__ __launch_bounds__(256) void k_nms_scan(const float* __restrict__ resp
         tot += (int)__popcll(m[u]);
     }
     if (tot == 0) return;
-    const int leader = 0;
     int base = 0;
-    if (lane_id() == (unsigned)leader) base = atomicAdd(&scan_count[f], tot);
-    base = __shfl(base, leader, 64);
+    if (lane_id() == 0u) base = atomicAdd(&scan_count[f], tot);
+    base = __shfl(base, 0, 64);
 #pragma unroll
     for (int u = 0; u < NU; u++) {
         if (ok[u]) {
@@ -1100,50 +1109,114 @@ __global__ __launch_bounds__(256) void k_nms_scan(const float* __restrict__ resp
     }
 }
 
-// Pass 2: interpolation + makePoint, one lane per survivor (no divergence
-// against the ~99 % of blocks that fail the 3x3x3 test).
+__global__ __launch_bounds__(256) void k_nms_scan(const float* __restrict__ resp, FrameParams P,
+                                                  const OctaveParams* __restrict__ oct, LaunchPlan plan,
+                                                  uint32_t* __restrict__ scan_key, uint32_t* __restrict__ scan_src,
+                                                  int* __restrict__ scan_count, int scap, int nframes)
+{
+    int f, gb;
+    if (!xcd_frame_block(plan.nms_start[kMaxOct], nframes, f, gb)) return;
+    nms_scan_item(resp, P, oct, plan, scan_key, scan_src, scan_count, scap, f, gb,
+                  __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+}
+
+// Exclusive prefix of min(count[f], cap) over the frames (one workgroup).
+__global__ __launch_bounds__(1024) void k_prefix_clamped(const int* __restrict__ counts, int nframes, int cap,
+                                                         int* __restrict__ offsets)
+{
+    __shared__ int part[1024];
+    const int per = (nframes + 1023) / 1024;
+    const int b = threadIdx.x * per;
+    int sum = 0;
+    for (int i = 0; i < per; i++) if (b + i < nframes) sum += min(counts[b + i], cap);
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int run = 0;
+        for (int t = 0; t < 1024; t++) { const int v = part[t]; part[t] = run; run += v; }
+        offsets[nframes] = run;
+    }
+    __syncthreads();
+    int run = part[threadIdx.x];
+    for (int i = 0; i < per; i++)
+        if (b + i < nframes) { offsets[b + i] = run; run += min(counts[b + i], cap); }
+}
+
+constexpr int kFitGrid = 1024;
+
+// Pass 2: interpolation + makePoint, one lane per survivor of the whole batch
+// (grid-stride over the prefix of the frames' survivor counts), so no lane
+// idles on the ~99 % of blocks that fail the 3x3x3 test and no workgroup is
+// launched for empty space.
 __global__ __launch_bounds__(256) void k_nms_fit(const int32_t* __restrict__ ii, const float* __restrict__ resp,
                                                  FrameParams P, const OctaveParams* __restrict__ oct,
                                                  const uint32_t* __restrict__ scan_key,
                                                  const uint32_t* __restrict__ scan_src,
-                                                 const int* __restrict__ scan_count, int scap,
+                                                 const int* __restrict__ scan_count, const int* __restrict__ soff,
+                                                 int scap, int nframes,
                                                  surfhip_point* __restrict__ cand, uint32_t* __restrict__ keys,
                                                  int* __restrict__ cand_count, int cap, int* status)
 {
-    const int f = blockIdx.y;
-    const int n = scan_count[f];
-    if (blockIdx.x == 0 && threadIdx.x == 0 && n > scap) atomicOr(status, 4);
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    if (blockIdx.x * 256 >= min(n, scap)) return;            // whole block idle
-    surfhip_point pt;
-    bool ok = false;
-    uint32_t key = 0;
-    if (t < min(n, scap)) {
-        key = scan_key[(size_t)f * scap + t];
-        const uint32_t src = scan_src[(size_t)f * scap + t];
-        const int o = (int)(key >> 29);
-        const OctaveParams& q = oct[o];
-        const OctView V = make_view(resp + (size_t)f * P.resp_stride, q, o);
-        const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
-        ok = nms_fit_point(I, V, P, q, o, (int)(src >> 28), (int)((src >> 14) & 0x3fffu), (int)(src & 0x3fffu), pt);
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
+        for (int f = threadIdx.x; f < nframes; f += 64)
+            if (scan_count[f] > scap) atomicOr(status, 4);
     }
-    const int slot = wave_append(ok, &cand_count[f]);
-    if (slot >= 0 && slot < cap) {
-        cand[(size_t)f * cap + slot] = pt;
-        keys[(size_t)f * cap + slot] = key;
+    const int total = soff[nframes];
+    const int stride = kFitGrid * 256;
+    for (int base = blockIdx.x * 256 + (threadIdx.x & ~63); base < total; base += stride) {
+        const int t = base + (int)lane_id();
+        const bool act = t < total;
+        int f = 0;
+        if (act) {                                   // frame of survivor t
+            int lo = 0, hi = nframes;
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (soff[mid] <= t) lo = mid; else hi = mid;
+            }
+            f = lo;
+        }
+        surfhip_point pt;
+        bool ok = false;
+        uint32_t key = 0;
+        if (act) {
+            const size_t src_i = (size_t)f * scap + (t - soff[f]);
+            key = scan_key[src_i];
+            const uint32_t src = scan_src[src_i];
+            const int o = (int)(key >> 29);
+            const OctaveParams& q = oct[o];
+            const OctView V = make_view(resp + (size_t)f * P.resp_stride, q, o);
+            const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
+            ok = nms_fit_point(I, V, P, q, o, (int)(src >> 28), (int)((src >> 14) & 0x3fffu), (int)(src & 0x3fffu), pt);
+        }
+        // a wave spans at most a few frames: append frame by frame
+        bool pending = ok;
+        while (__ballot(pending)) {
+            const int leader = __builtin_ctzll(__ballot(pending));
+            const int ff = __shfl(f, leader, 64);
+            const bool mine = pending && f == ff;
+            const int slot = wave_append(mine, &cand_count[ff]);
+            if (mine) {
+                if (slot < cap) {
+                    cand[(size_t)ff * cap + slot] = pt;
+                    keys[(size_t)ff * cap + slot] = key;
+                }
+                pending = false;
+            }
+        }
     }
 }
 
 hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,
                       const OctaveParams* d_oct, const LaunchPlan& plan, uint32_t* scan_key, uint32_t* scan_src,
                       int* scan_count, int scap, surfhip_point* cand, uint32_t* keys, int* cand_count, int cap,
-                      int* status, hipStream_t s)
+                      int* status, int* scratch_off, hipStream_t s)
 {
     if (plan.nms_start[kMaxOct] == 0) return hipSuccess;
     k_nms_scan<<<dim3(((nframes + 7) & ~7) * plan.nms_start[kMaxOct]), 256, 0, s>>>(resp, P, d_oct, plan, scan_key,
                                                                                      scan_src, scan_count, scap, nframes);
-    k_nms_fit<<<dim3((scap + 255) / 256, nframes), 256, 0, s>>>(ii, resp, P, d_oct, scan_key, scan_src, scan_count,
-                                                                 scap, cand, keys, cand_count, cap, status);
+    k_prefix_clamped<<<1, 1024, 0, s>>>(scan_count, nframes, scap, scratch_off);
+    k_nms_fit<<<kFitGrid, 256, 0, s>>>(ii, resp, P, d_oct, scan_key, scan_src, scan_count, scratch_off, scap, nframes,
+                                       cand, keys, cand_count, cap, status);
     return hipGetLastError();
 }
 
@@ -1176,7 +1249,7 @@ __global__ __launch_bounds__(1024) void k_sort(const surfhip_point* __restrict__
                                                const uint32_t* __restrict__ keys,
                                                uint64_t* __restrict__ gscratch, int* cand_count, int cap,
                                                surfhip_point* __restrict__ out, int max_pts,
-                                               int* __restrict__ out_count, int* status)
+                                               int* __restrict__ out_count, int* __restrict__ order, int* status)
 {
     extern __shared__ __attribute__((aligned(16))) uint64_t sk[];
     const int f = blockIdx.x;
@@ -1201,6 +1274,10 @@ __global__ __launch_bounds__(1024) void k_sort(const surfhip_point* __restrict__
     for (int t = threadIdx.x; t < keep; t += blockDim.x)
         out[(size_t)f * max_pts + t] = cand[(size_t)f * cap + (uint32_t)(s[t] & 0xffffffffu)];
     if (threadIdx.x == 0) out_count[f] = keep;
+    // Describe schedule (processing order only; descriptors land at their
+    // canonical index).  Canonical order: row-ordered schedules measured no
+    // faster (the descriptor is bound by texture-address work, not L2).
+    for (int t = threadIdx.x; t < keep; t += blockDim.x) order[(size_t)f * max_pts + t] = t;
 }
 
 __global__ __launch_bounds__(1024) void k_offsets(const int* __restrict__ counts, int nframes, int* __restrict__ offsets)
@@ -1225,7 +1302,7 @@ __global__ __launch_bounds__(1024) void k_offsets(const int* __restrict__ counts
 
 hipError_t launch_sort(const surfhip_point* cand, const uint32_t* keys, uint64_t* gscratch,
                        int* cand_count, int cap, int nframes, surfhip_point* out, int max_pts,
-                       int* out_count, int* offsets, int* status, hipStream_t s)
+                       int* out_count, int* offsets, int* order, int* status, hipStream_t s)
 {
     static bool attr_set = false;
     if (!attr_set) {
@@ -1236,7 +1313,7 @@ hipError_t launch_sort(const surfhip_point* cand, const uint32_t* keys, uint64_t
         attr_set = true;
     }
     k_sort<<<nframes, 1024, kSortCap * sizeof(uint64_t), s>>>(cand, keys, gscratch, cand_count, cap, out,
-                                                              max_pts, out_count, status);
+                                                              max_pts, out_count, order, status);
     k_offsets<<<1, 1024, 0, s>>>(out_count, nframes, offsets);
     return hipGetLastError();
 }
@@ -1477,7 +1554,7 @@ template <bool UPRIGHT>
 __global__ __launch_bounds__(256) void k_describe(const int32_t* __restrict__ ii, FrameParams P,
                                                   surfhip_point* __restrict__ pts, int max_pts,
                                                   const int* __restrict__ counts, const int* __restrict__ offsets,
-                                                  int nframes, float* __restrict__ desc)
+                                                  const int* __restrict__ order, int nframes, float* __restrict__ desc)
 {
     __shared__ float sdesc[4][128];
     __shared__ OriScratch sori[UPRIGHT ? 1 : 4];
@@ -1494,7 +1571,7 @@ __global__ __launch_bounds__(256) void k_describe(const int32_t* __restrict__ ii
             const int mid = (lo + hi) >> 1;
             if (offsets[mid] <= g) lo = mid; else hi = mid;
         }
-        const int f = lo, i = g - offsets[lo];
+        const int f = lo, i = order[(size_t)lo * max_pts + (g - offsets[lo])];
         surfhip_point* pp = pts + (size_t)f * max_pts + i;
         const surfhip_point p = *pp;
         const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
@@ -1622,7 +1699,8 @@ template <int R> struct IntC { static constexpr int value = R; };
 template <bool EXT>
 __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__ ii, FrameParams P,
                                                      const surfhip_point* __restrict__ pts, int max_pts,
-                                                     const int* __restrict__ offsets, int nframes,
+                                                     const int* __restrict__ offsets,
+                                                     const int* __restrict__ order, int nframes,
                                                      float* __restrict__ desc)
 {
     constexpr int WSZ = 4;
@@ -1652,7 +1730,7 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
     // the current one is described
     const int gstride = nbx * 4;
     int gn = gbeg + lb * 4 + w;
-    int fn = 0, fnb = 0, fne = 0;
+    int fn = 0, fnb = 0, fne = 0, kn = 0;
     surfhip_point pn;
     if (gn < gend) {
         int lo = 0, hi = nframes;
@@ -1663,15 +1741,17 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
         fn = lo;
         fnb = offsets[lo];
         fne = offsets[lo + 1];
-        pn = pts[(size_t)fn * max_pts + (gn - fnb)];
+        kn = order[(size_t)fn * max_pts + (gn - fnb)];
+        pn = pts[(size_t)fn * max_pts + kn];
     }
     while (gn < gend) {
-        const int f = fn, kp = gn - fnb;
+        const int f = fn, kp = kn;
         const surfhip_point p = pn;
         gn += gstride;
         if (gn < gend) {
             while (gn >= fne) { fn++; fnb = fne; fne = offsets[fn + 1]; }
-            pn = pts[(size_t)fn * max_pts + (gn - fnb)];
+            kn = order[(size_t)fn * max_pts + (gn - fnb)];
+            pn = pts[(size_t)fn * max_pts + kn];
         }
         const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
         const __amdgpu_buffer_rsrc_t rsrc = frame_rsrc(I, P.ii_stride * 4);
@@ -1822,17 +1902,18 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
 }
 
 hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
-                           const int* counts, const int* offsets, int nframes, float* desc, hipStream_t s)
+                           const int* counts, const int* offsets, const int* order, int nframes, float* desc,
+                           hipStream_t s)
 {
     if (P.nfeat > 128) return hipErrorInvalidValue;
     const int grid = 2048;
     if (P.upright && P.wsz == 4) {
-        if (P.extend) k_describe_ur<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, nframes, desc);
-        else k_describe_ur<false><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, nframes, desc);
+        if (P.extend) k_describe_ur<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc);
+        else k_describe_ur<false><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc);
     } else if (P.upright) {
-        k_describe<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, counts, offsets, nframes, desc);
+        k_describe<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, counts, offsets, order, nframes, desc);
     } else {
-        k_describe<false><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, counts, offsets, nframes, desc);
+        k_describe<false><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, counts, offsets, order, nframes, desc);
     }
     return hipGetLastError();
 }
