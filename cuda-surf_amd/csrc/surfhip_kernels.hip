@@ -43,6 +43,14 @@ __device__ __forceinline__ unsigned lane_id()
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
 
+// LDS visibility between the lanes of one wave
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ======================================================================
 // Integral image.  Three passes over row bands of kBandRows rows:
 //  (A) k_ii_bandsum : per band, per column, the sum of the band's pixels
@@ -883,60 +891,6 @@ __device__ __forceinline__ int32_t trace_sign(const uint32_t* __restrict__ I, in
     return ((int32_t)((uint32_t)lxx + (uint32_t)lyy) > 0) ? 1 : -1;
 }
 
-// 3x3x3 scale-space maximum test of one 2x2x2 block (surfd.cu:678-792):
-// on success returns the block's argmax (s, r, c).
-__device__ __forceinline__ bool nms_scan_block(const OctView& V, const FrameParams& P, const OctaveParams& q, int z,
-                                               int x, int y, int& s_out, int& r_out, int& c_out)
-{
-    const int sw = q.sw, sh = q.sh;
-    const int k = 2 * z + 1;
-    const int mb = q.mb[z];
-    const int i = mb + y * 2;
-    const int j = mb + x * 2;
-    if (i >= sh - mb || j >= sw - mb) return false;
-
-    // argmax over the 2x2x2 block, order (k: w,x,y,z; k+1: w,x,y,z), strict '>'
-    int cas = 0;
-    float best = V(k, i, j), t;
-    if ((t = V(k, i, j + 1)) > best) { best = t; cas = 1; }
-    if ((t = V(k, i + 1, j)) > best) { best = t; cas = 2; }
-    if ((t = V(k, i + 1, j + 1)) > best) { best = t; cas = 3; }
-    if ((t = V(k + 1, i, j)) > best) { best = t; cas = 4; }
-    if ((t = V(k + 1, i, j + 1)) > best) { best = t; cas = 5; }
-    if ((t = V(k + 1, i + 1, j)) > best) { best = t; cas = 6; }
-    if ((t = V(k + 1, i + 1, j + 1)) > best) { best = t; cas = 7; }
-    if (best < P.thresh * 0.8f || (k + 1 == P.max_scale - 1 && cas > 3)) return false;
-
-    int s = k, r = i, c = j, ds = -1, dr = -1, dc = -1;
-    if (cas != 0) {
-        if (cas == 1) { c = j + 1; dc = 1; }
-        else if (cas == 2) { r = i + 1; dr = 1; }
-        else if (cas == 3) { c = j + 1; r = i + 1; dc = 1; dr = 1; }
-        else {
-            s++; ds = 1;
-            if (cas == 5) { c = j + 1; dc = 1; }
-            else if (cas == 6) { r = i + 1; dr = 1; }
-            else if (cas == 7) { c = j + 1; r = i + 1; dc = 1; dr = 1; }
-        }
-    }
-    // the 19 neighbours outside the block (surfd.cu:757-792); ties survive
-    const int so = s + ds, si = s - ds;
-#pragma unroll
-    for (int rr = -1; rr <= 1; rr++) {
-        const int row = r + rr * dr;
-        if (best < V(so, row, c - 1) || best < V(so, row, c) || best < V(so, row, c + 1)) return false;
-    }
-    const int rn = r + dr, rp = r - dr, cn = c + dc;
-    if (best < V(s, rn, c - 1) || best < V(s, rn, c) || best < V(s, rn, c + 1)) return false;
-    if (best < V(s, r, cn) || best < V(s, rp, cn)) return false;
-    if (best < V(si, rn, c - 1) || best < V(si, rn, c) || best < V(si, rn, c + 1)) return false;
-    if (best < V(si, rp, cn) || best < V(si, r, cn)) return false;
-    s_out = s;
-    r_out = r;
-    c_out = c;
-    return true;
-}
-
 // Sub-pixel interpolation + acceptance + makePoint (surfd.cu:794-831,
 // 942-1022) for one NMS survivor.
 __device__ bool nms_fit_point(const uint32_t* __restrict__ I, const OctView& V, const FrameParams& P,
@@ -1028,7 +982,8 @@ __device__ __forceinline__ int wave_append(bool ok, int* counter)
 __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, const FrameParams& P,
                                               const OctaveParams* __restrict__ oct, const LaunchPlan& plan,
                                               uint32_t* __restrict__ scan_key, uint32_t* __restrict__ scan_src,
-                                              int* __restrict__ scan_count, int scap, int f, int gb, int wv)
+                                              int* __restrict__ scan_count, int scap, int f, int gb, int wv,
+                                              float* sbest, uint32_t* sinfo)
 {
     constexpr int NU = kScanRows / 4;        // block rows per lane
     const int o = octave_of(plan.nms_start, P.noct, gb);
@@ -1055,9 +1010,12 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
         V.pair(k + 1, ii, jj, v[u][4], v[u][5]);
         V.pair(k + 1, ii + 1, jj, v[u][6], v[u][7]);
     }
-    // ---- argmax + threshold, then the 19 outer neighbours for the rare survivors
-    bool ok[NU];
-    int ss[NU], rr[NU], cc[NU];
+    // ---- argmax over the 2x2x2 block in the reference's order (k: w,x,y,z;
+    // k+1: w,x,y,z), strict '>', threshold and top-scale rejection
+    // (surfd.cu:678-756)
+    bool cnd[NU];
+    float bst[NU];
+    int cs[NU];
 #pragma unroll
     for (int u = 0; u < NU; u++) {
         int cas = 0;
@@ -1065,48 +1023,63 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
 #pragma unroll
         for (int t = 1; t < 8; t++)
             if (v[u][t] > best) { best = v[u][t]; cas = t; }
-        const int i = mb + (y0 + 4 * u) * 2;
-        ok[u] = in[u] && !(best < P.thresh * 0.8f || (k + 1 == P.max_scale - 1 && cas > 3));
-        int s = k + (cas >> 2), r = i + ((cas >> 1) & 1), c = j + (cas & 1);
-        ss[u] = s; rr[u] = r; cc[u] = c;
-        if (ok[u]) {
+        cnd[u] = in[u] && !(best < P.thresh * 0.8f || (k + 1 == P.max_scale - 1 && cas > 3));
+        bst[u] = best;
+        cs[u] = cas;
+    }
+    // ---- compact the candidates of all NU rows into dense lanes (LDS), so
+    // the 19-neighbour test costs 19 loads per 64 candidates, not per row
+    unsigned long long m[NU];
+    int ncand = 0;
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+        m[u] = __ballot(cnd[u]);
+        if (cnd[u]) {
+            const int slot = ncand + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m[u] >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((unsigned)m[u], 0u));
+            sbest[slot] = bst[u];
+            sinfo[slot] = ((uint32_t)u << 9) | ((uint32_t)cs[u] << 6) | lane_id();
+        }
+        ncand += (int)__popcll(m[u]);
+    }
+    if (ncand == 0) return;
+    wave_sync();
+    const int bx0 = (lb % nbx) * 64;
+    for (int c0 = 0; c0 < ncand; c0 += 64) {
+        const int ci = c0 + (int)lane_id();
+        bool ok = false;
+        int s = 0, r = 0, c = 0, x = 0, y = 0;
+        if (ci < ncand) {
+            const float best = sbest[ci];
+            const uint32_t info = sinfo[ci];
+            const int u = (int)(info >> 9), cas = (int)((info >> 6) & 7u);
+            x = bx0 + (int)(info & 63u);
+            y = y0 + 4 * u;
+            const int i = mb + y * 2, j = mb + x * 2;
+            s = k + (cas >> 2); r = i + ((cas >> 1) & 1); c = j + (cas & 1);
             const int ds = (cas >> 2) ? 1 : -1, dr = ((cas >> 1) & 1) ? 1 : -1, dc = (cas & 1) ? 1 : -1;
             const int so = s + ds, si = s - ds;
             const int rn = r + dr, rp = r - dr, cn = c + dc;
-            ok[u] = !(best < V(so, rp, c - 1) || best < V(so, rp, c) || best < V(so, rp, c + 1) ||
-                      best < V(so, r, c - 1) || best < V(so, r, c) || best < V(so, r, c + 1) ||
-                      best < V(so, rn, c - 1) || best < V(so, rn, c) || best < V(so, rn, c + 1) ||
-                      best < V(s, rn, c - 1) || best < V(s, rn, c) || best < V(s, rn, c + 1) ||
-                      best < V(s, r, cn) || best < V(s, rp, cn) ||
-                      best < V(si, rn, c - 1) || best < V(si, rn, c) || best < V(si, rn, c + 1) ||
-                      best < V(si, rp, cn) || best < V(si, r, cn));
+            // the 19 neighbours outside the block, ties survive (surfd.cu:757-792);
+            // all loads issued before any compare
+            const float nb[19] = {V(so, rp, c - 1), V(so, rp, c), V(so, rp, c + 1),
+                                  V(so, r, c - 1),  V(so, r, c),  V(so, r, c + 1),
+                                  V(so, rn, c - 1), V(so, rn, c), V(so, rn, c + 1),
+                                  V(s, rn, c - 1),  V(s, rn, c),  V(s, rn, c + 1),
+                                  V(s, r, cn),      V(s, rp, cn),
+                                  V(si, rn, c - 1), V(si, rn, c), V(si, rn, c + 1),
+                                  V(si, rp, cn),    V(si, r, cn)};
+            ok = true;
+#pragma unroll
+            for (int t = 0; t < 19; t++) ok = ok && !(best < nb[t]);
+        }
+        const int slot = wave_append(ok, &scan_count[f]);
+        if (ok && slot < scap) {
+            scan_key[(size_t)f * scap + slot] = ((uint32_t)o << 29) | ((uint32_t)z << 28) | ((uint32_t)y << 14) | (uint32_t)x;
+            scan_src[(size_t)f * scap + slot] = ((uint32_t)s << 28) | ((uint32_t)r << 14) | (uint32_t)c;
         }
     }
-    // ---- one atomic per wave for all its survivors
-    unsigned long long m[NU];
-    int tot = 0;
-#pragma unroll
-    for (int u = 0; u < NU; u++) {
-        m[u] = __ballot(ok[u]);
-        tot += (int)__popcll(m[u]);
-    }
-    if (tot == 0) return;
-    int base = 0;
-    if (lane_id() == 0u) base = atomicAdd(&scan_count[f], tot);
-    base = __shfl(base, 0, 64);
-#pragma unroll
-    for (int u = 0; u < NU; u++) {
-        if (ok[u]) {
-            const int slot = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m[u] >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((unsigned)m[u], 0u));
-            if (slot < scap) {
-                const int y = y0 + 4 * u;
-                scan_key[(size_t)f * scap + slot] = ((uint32_t)o << 29) | ((uint32_t)z << 28) | ((uint32_t)y << 14) | (uint32_t)x;
-                scan_src[(size_t)f * scap + slot] = ((uint32_t)ss[u] << 28) | ((uint32_t)rr[u] << 14) | (uint32_t)cc[u];
-            }
-        }
-        base += (int)__popcll(m[u]);
-    }
+    wave_sync();
 }
 
 __global__ __launch_bounds__(256) void k_nms_scan(const float* __restrict__ resp, FrameParams P,
@@ -1114,10 +1087,12 @@ __global__ __launch_bounds__(256) void k_nms_scan(const float* __restrict__ resp
                                                   uint32_t* __restrict__ scan_key, uint32_t* __restrict__ scan_src,
                                                   int* __restrict__ scan_count, int scap, int nframes)
 {
+    __shared__ float sbest[4][64 * (kScanRows / 4)];
+    __shared__ uint32_t sinfo[4][64 * (kScanRows / 4)];
     int f, gb;
     if (!xcd_frame_block(plan.nms_start[kMaxOct], nframes, f, gb)) return;
-    nms_scan_item(resp, P, oct, plan, scan_key, scan_src, scan_count, scap, f, gb,
-                  __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    nms_scan_item(resp, P, oct, plan, scan_key, scan_src, scan_count, scap, f, gb, wv, sbest[wv], sinfo[wv]);
 }
 
 // Exclusive prefix of min(count[f], cap) over the frames (one workgroup).
@@ -1418,12 +1393,6 @@ __device__ __forceinline__ void place(float* d, int wsz, int osz, float mag1, in
     }
 }
 
-__device__ __forceinline__ void wave_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 struct OriScratch {
     int   hid[361];
@@ -1710,6 +1679,7 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
     __shared__ float red[4][64][RS];
     __shared__ float s_cf[4][64];
     __shared__ float s_rf[4][64], s_rp[4][64];
+    __shared__ int s_ri[4][64];
     __shared__ unsigned long long s_mask[4][6];
     __shared__ float s_lut[40];
     if (threadIdx.x < 40) s_lut[threadIdx.x] = c_tab.lut2[threadIdx.x];
@@ -1774,6 +1744,7 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
         const int ri_t = f2i_rz(rx_t >= 0.f ? rx_t : rx_t - 1.f);
         s_rf[w][lane] = rx_t - (float)ri_t;
         s_rp[w][lane] = rpos_t * rpos_t;
+        s_ri[w][lane] = ri_t;
         // ---- grid column of this lane
         const int j = dual ? (lane & 31) : lane;
         const int h = dual ? (lane >> 5) : 0;
@@ -1796,28 +1767,43 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
         for (int R = 0; R < WSZ; R++)
 #pragma unroll
             for (int s = 0; s < NS; s++) acc[R][s] = 0.f;
-        auto band = [&](auto Rc) {
-            constexpr int R = decltype(Rc)::value;
-            const unsigned long long m = __ballot(rvalid && ri_t == R);
-            if (m == 0ull) return;
-            const int r0 = __builtin_ctzll(m), n = __builtin_popcountll(m);
-            float Ps[NS], Qs[NS];
+        // ---- the valid grid rows form one contiguous run [t0, t0 + nv); half h
+        // takes rows t0 + h, t0 + h + rstep, ...  Rows go in batches of DU with
+        // all their loads issued first (the loop is latency-bound otherwise).
+        // A row adds S * (1 - rfrac) to cell row ri and S * rfrac to ri + 1
+        // (placeInIndex, surfd.cu:1199-1271); the weights of the 4 cell rows
+        // are formed by selects, so the accumulators keep fixed registers.
+        const unsigned long long vm = __ballot(rvalid);
+        const int t0 = vm ? __builtin_ctzll(vm) : 0, nv = __builtin_popcountll(vm);
+        constexpr int DU = 3;
+        for (int k0 = h; k0 < nv; k0 += DU * rstep) {
+            uint32_t A[DU][12];
 #pragma unroll
-            for (int s = 0; s < NS; s++) Ps[s] = Qs[s] = 0.f;
-            if (col_on) {
-                for (int k = h; k < n; k += rstep) {
-                    const int tt = r0 + k;
-                    const float rf = s_rf[w][tt];
-                    const float rp = s_rp[w][tt];
-                    const int rb = (iy + (tt - iradius) * step) * ip4;
+            for (int u = 0; u < DU; u++) {
+                const int k = k0 + u * rstep;
+                if (col_on && k < nv) {
+                    const int rb = (iy + (t0 + k - iradius) * step) * ip4;
                     const int q0 = rb + dR0, q2 = rb + ip4, q3 = rb + dR3;
                     // corners (row, col): rows r-s, r, r+1, r+s+1; cols c-s, c+s+1, c, c+1
-                    const uint32_t a00 = bld(rsrc, q0 + oA), a01 = bld(rsrc, q0 + oB);
-                    const uint32_t a02 = bld(rsrc, q0 + oC), a03 = bld(rsrc, q0 + oC + 4);
-                    const uint32_t a10 = bld(rsrc, rb + oA), a11 = bld(rsrc, rb + oB);
-                    const uint32_t a20 = bld(rsrc, q2 + oA), a21 = bld(rsrc, q2 + oB);
-                    const uint32_t a30 = bld(rsrc, q3 + oA), a31 = bld(rsrc, q3 + oB);
-                    const uint32_t a32 = bld(rsrc, q3 + oC), a33 = bld(rsrc, q3 + oC + 4);
+                    A[u][0] = bld(rsrc, q0 + oA);  A[u][1] = bld(rsrc, q0 + oB);
+                    A[u][2] = bld(rsrc, q0 + oC);  A[u][3] = bld(rsrc, q0 + oC + 4);
+                    A[u][4] = bld(rsrc, rb + oA);  A[u][5] = bld(rsrc, rb + oB);
+                    A[u][6] = bld(rsrc, q2 + oA);  A[u][7] = bld(rsrc, q2 + oB);
+                    A[u][8] = bld(rsrc, q3 + oA);  A[u][9] = bld(rsrc, q3 + oB);
+                    A[u][10] = bld(rsrc, q3 + oC); A[u][11] = bld(rsrc, q3 + oC + 4);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < DU; u++) {
+                const int k = k0 + u * rstep;
+                if (col_on && k < nv) {
+                    const int tt = t0 + k;
+                    const float rf = s_rf[w][tt];
+                    const float rp = s_rp[w][tt];
+                    const int ri = s_ri[w][tt];
+                    const uint32_t a00 = A[u][0], a01 = A[u][1], a02 = A[u][2], a03 = A[u][3];
+                    const uint32_t a10 = A[u][4], a11 = A[u][5], a20 = A[u][6], a21 = A[u][7];
+                    const uint32_t a30 = A[u][8], a31 = A[u][9], a32 = A[u][10], a33 = A[u][11];
                     // haarX / haarY (surfd.cu:1171-1182 via getSum)
                     const int32_t wav1 = (int32_t)((a21 + a00 - a01 - a20) - (a31 + a10 - a11 - a30));
                     const int32_t wav2 = (int32_t)((a31 + a02 - a01 - a32) - (a33 + a00 - a03 - a30));
@@ -1835,24 +1821,16 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
                         S[4] = dy;  S[5] = dx < 0.f ? dy : 0.f;    // bins 5 | 4 by sign of dx
                         S[6] = ady; S[7] = dx < 0.f ? ady : 0.f;   // bins 7 | 6
                     }
+                    const float w0 = 1.f - rf;
 #pragma unroll
-                    for (int s = 0; s < NS; s++) {
-                        Ps[s] += S[s];
-                        Qs[s] = fmaf(S[s], rf, Qs[s]);
+                    for (int R = 0; R < WSZ; R++) {
+                        const float rw = (R == ri) ? w0 : ((R == ri + 1) ? rf : 0.f);
+#pragma unroll
+                        for (int s = 0; s < NS; s++) acc[R][s] = fmaf(S[s], rw, acc[R][s]);
                     }
                 }
             }
-#pragma unroll
-            for (int s = 0; s < NS; s++) {
-                if constexpr (R >= 0) acc[R][s] += Ps[s] - Qs[s];
-                if constexpr (R + 1 < WSZ) acc[R + 1][s] += Qs[s];
-            }
-        };
-        band(IntC<-1>{});
-        band(IntC<0>{});
-        band(IntC<1>{});
-        band(IntC<2>{});
-        band(IntC<3>{});
+        }
         // ---- per-lane bins, then the fixed-order column reduction
 #pragma unroll
         for (int R = 0; R < WSZ; R++)
