@@ -254,7 +254,8 @@ def main():
             "keypoints_per_s": round(kp_total_batch * args.steps / elapsed, 1),
             "keypoints_per_frame": round(kp_total_batch / (world * B), 1),
             "stage_ms_per_step": {k: round(v / args.steps, 4) for k, v in stage_acc.items()},
-            "roofline": {"kernel": "Hessian stage: k_hess_o0 (octave 0) + k_hessian (octaves >= 1), per batch",
+            "roofline": {"kernel": "Hessian stage: k_hess_o0 (octave 0) + k_hess_o1 (octave 1) + k_hessian "
+                                   "(octaves >= 2), per batch",
                          "bound": "hbm",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),

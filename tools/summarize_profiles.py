@@ -58,14 +58,17 @@ def main():
             wr = rows.get((k, "WRITE_SIZE"), [0.0])
             fm, wm = sum(f) / len(f), sum(wr) / len(wr)
             w.writerow([k, len(f), round(fm, 2), round(wm, 2), int((2 * fm + wm) * 1024)])
-    hf = rows[("k_hessian", "FETCH_SIZE")]
-    hw = rows[("k_hessian", "WRITE_SIZE")]
-    fm, wm = sum(hf) / len(hf), sum(hw) / len(hw)
+    # the Hessian stage = every launch whose name starts with k_hess (octave 0
+    # ring, octave 1 ring, gather kernel for octaves >= 2): per-batch sums
+    hk = [k for k in kernels if k.startswith("k_hess")]
+    fm = sum(sum(rows[(k, "FETCH_SIZE")]) / len(rows[(k, "FETCH_SIZE")]) for k in hk)
+    wm = sum(sum(rows[(k, "WRITE_SIZE")]) / len(rows[(k, "WRITE_SIZE")]) for k in hk)
     out = {"config": f"{args.batch}x{args.width}x{args.height}x{args.octaves}", "tag": t,
-           "kernel": "k_hessian", "fetch_kib": fm, "write_kib": wm,
+           "kernel": "+".join(hk), "fetch_kib": fm, "write_kib": wm,
            "bytes_per_launch": (2 * fm + wm) * 1024,
            "note": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes over "
-                   "`bench.py --hessian-only`; traffic = (2*FETCH_SIZE + WRITE_SIZE) KiB (gfx950 correction)"}
+                   "`bench.py --hessian-only`; traffic = (2*FETCH_SIZE + WRITE_SIZE) KiB (gfx950 "
+                   "correction), summed over the Hessian stage's kernels per batch"}
     with open(os.path.join(prof, "hessian_pmc.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
