@@ -424,8 +424,9 @@ __device__ __forceinline__ void hess_store(const lds_u64* Tl, int sb, const Octa
     const int b1 = q.b1[S];
     const bool vy = iy >= b1 && iy < q.sh - b1;
     float* pl = row + (size_t)S * q.osize;
-    if (ixa < q.sw) pl[ixa] = (vy && ixa >= b1 && ixa < q.sw - b1) ? ha : 0.f;
-    if (ixb < q.sw) pl[ixb] = (vy && ixb >= b1 && ixb < q.sw - b1) ? hb : 0.f;
+    // streaming stores: the planes are read back only by the NMS pass
+    if (ixa < q.sw) __builtin_nontemporal_store((vy && ixa >= b1 && ixa < q.sw - b1) ? ha : 0.f, pl + ixa);
+    if (ixb < q.sw) __builtin_nontemporal_store((vy && ixb >= b1 && ixb < q.sw - b1) ? hb : 0.f, pl + ixb);
 }
 
 // One fill item: image row gy, columns xs + 4a .. + 3 and the same + 128.
@@ -642,7 +643,7 @@ __global__ __launch_bounds__(o1::THREADS, 1) void k_hess_o1(const int32_t* __res
             else if (us == 1) h = hess1<19, 9, 18, 27>(Tl, sb, norm);
             else h = hess1<23, 11, 22, 33>(Tl, sb, norm);
             const bool v = iy >= b1 && iy < q.sh - b1 && ix >= b1 && ix < q.sw - b1;
-            if (ix < q.sw) plane[(size_t)iy * q.sp + ix] = v ? h : 0.f;
+            if (ix < q.sw) __builtin_nontemporal_store(v ? h : 0.f, plane + (size_t)iy * q.sp + ix);
         }
         if (s + 1 < nsteps) {
             const int yw = 16 * s + 48;
