@@ -1776,59 +1776,90 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
         // are formed by selects, so the accumulators keep fixed registers.
         const unsigned long long vm = __ballot(rvalid);
         const int t0 = vm ? __builtin_ctzll(vm) : 0, nv = __builtin_popcountll(vm);
-        constexpr int DU = 3;
-        for (int k0 = h; k0 < nv; k0 += DU * rstep) {
-            uint32_t A[DU][12];
+        // one sample: its 12 integral-image corners -> haar responses -> bins
+        auto accum = [&](uint32_t a00, uint32_t a01, uint32_t a02, uint32_t a03, uint32_t a10, uint32_t a11,
+                         uint32_t a20, uint32_t a21, uint32_t a30, uint32_t a31, uint32_t a32, uint32_t a33,
+                         int tt) {
+            const float rf = s_rf[w][tt];
+            const float rp = s_rp[w][tt];
+            const int ri = s_ri[w][tt];
+            // haarX / haarY (surfd.cu:1171-1182 via getSum); rows r-s, r, r+1,
+            // r+s+1 (a0*, a1*, a2*, a3*), cols c-s, c+s+1, c, c+1
+            const int32_t wav1 = (int32_t)((a21 + a00 - a01 - a20) - (a31 + a10 - a11 - a30));
+            const int32_t wav2 = (int32_t)((a31 + a02 - a01 - a32) - (a33 + a00 - a03 - a30));
+            const float weight = s_lut[f2i_rz(rp + cp2)];
+            const float dx = (weight * (float)wav2) * INV255;
+            const float dy = (weight * (float)wav1) * INV255;
+            float S[NS];
+            if constexpr (!EXT) {
+                S[0] = dx; S[1] = fminf(dx, 0.f);          // bins 1 | 0 by sign of dx
+                S[2] = dy; S[3] = fminf(dy, 0.f);          // bins 3 | 2 by sign of dy
+            } else {
+                const float adx = fabsf(dx), ady = fabsf(dy);
+                S[0] = dx;  S[1] = dy < 0.f ? dx : 0.f;    // bins 1 | 0 by sign of dy
+                S[2] = adx; S[3] = dy < 0.f ? adx : 0.f;   // bins 3 | 2
+                S[4] = dy;  S[5] = dx < 0.f ? dy : 0.f;    // bins 5 | 4 by sign of dx
+                S[6] = ady; S[7] = dx < 0.f ? ady : 0.f;   // bins 7 | 6
+            }
+            const float w0 = 1.f - rf;
 #pragma unroll
-            for (int u = 0; u < DU; u++) {
-                const int k = k0 + u * rstep;
-                if (col_on && k < nv) {
-                    const int rb = (iy + (t0 + k - iradius) * step) * ip4;
-                    const int q0 = rb + dR0, q2 = rb + ip4, q3 = rb + dR3;
-                    // corners (row, col): rows r-s, r, r+1, r+s+1; cols c-s, c+s+1, c, c+1
-                    A[u][0] = bld(rsrc, q0 + oA);  A[u][1] = bld(rsrc, q0 + oB);
-                    A[u][2] = bld(rsrc, q0 + oC);  A[u][3] = bld(rsrc, q0 + oC + 4);
-                    A[u][4] = bld(rsrc, rb + oA);  A[u][5] = bld(rsrc, rb + oB);
-                    A[u][6] = bld(rsrc, q2 + oA);  A[u][7] = bld(rsrc, q2 + oB);
-                    A[u][8] = bld(rsrc, q3 + oA);  A[u][9] = bld(rsrc, q3 + oB);
-                    A[u][10] = bld(rsrc, q3 + oC); A[u][11] = bld(rsrc, q3 + oC + 4);
+            for (int R = 0; R < WSZ; R++) {
+                const float rw = (R == ri) ? w0 : ((R == ri + 1) ? rf : 0.f);
+#pragma unroll
+                for (int s = 0; s < NS; s++) acc[R][s] = fmaf(S[s], rw, acc[R][s]);
+            }
+        };
+        const int hmode = hs - 2 * step;          // 0 or -1: the grid's rows share integral rows
+        if (hmode == 0 || hmode == -1) {
+            // ---- Row sharing.  step = rn(scale / 2) and hs = rz(scale) give
+            // hs = 2 step or 2 step - 1, so the outer rows r - hs and r + hs + 1
+            // of grid row i are rows r and r + 1 of grid rows i - 2 and i + 2.
+            // Each half walks every other grid row (dual: rows of its parity;
+            // single: even rows, then odd rows) keeping the (r, r + 1) rows of
+            // i - 2, i, i + 2 in registers: 8 loads per sample instead of 12.
+            const int nph = dual ? 1 : 2;
+            for (int ph = 0; ph < nph; ph++) {
+                const int hh = dual ? h : ph;
+                auto load8 = [&](int t, uint32_t (&T)[8]) {      // rows r, r+1 x cols c-s, c, c+1, c+s+1
+                    const int rb = (iy + (t - iradius) * step) * ip4, rb1 = rb + ip4;
+                    T[0] = bld(rsrc, rb + oA); T[1] = bld(rsrc, rb + oC); T[2] = bld(rsrc, rb + oC + 4);
+                    T[3] = bld(rsrc, rb + oB);
+                    T[4] = bld(rsrc, rb1 + oA); T[5] = bld(rsrc, rb1 + oC); T[6] = bld(rsrc, rb1 + oC + 4);
+                    T[7] = bld(rsrc, rb1 + oB);
+                };
+                uint32_t Pv[8], Cv[8], Nv[8];
+                const int tb = t0 + hh;
+                if (col_on && hh < nv) {
+                    load8(tb - 2, Pv);
+                    load8(tb, Cv);
+                }
+                for (int k = hh; k < nv; k += 2) {
+                    const int t = t0 + k;
+                    if (col_on) {
+                        load8(t + 2, Nv);
+                        const bool A = hmode == 0;
+                        // top row r - hs, bottom row r + hs + 1
+                        const uint32_t T0 = A ? Pv[0] : Pv[4], T1 = A ? Pv[1] : Pv[5];
+                        const uint32_t T2 = A ? Pv[2] : Pv[6], T3 = A ? Pv[3] : Pv[7];
+                        const uint32_t B0 = A ? Nv[4] : Nv[0], B1 = A ? Nv[5] : Nv[1];
+                        const uint32_t B2 = A ? Nv[6] : Nv[2], B3 = A ? Nv[7] : Nv[3];
+                        accum(T0, T3, T1, T2, Cv[0], Cv[3], Cv[4], Cv[7], B0, B3, B1, B2, t);
+#pragma unroll
+                        for (int e = 0; e < 8; e++) { Pv[e] = Cv[e]; Cv[e] = Nv[e]; }
+                    }
                 }
             }
-#pragma unroll
-            for (int u = 0; u < DU; u++) {
-                const int k = k0 + u * rstep;
-                if (col_on && k < nv) {
-                    const int tt = t0 + k;
-                    const float rf = s_rf[w][tt];
-                    const float rp = s_rp[w][tt];
-                    const int ri = s_ri[w][tt];
-                    const uint32_t a00 = A[u][0], a01 = A[u][1], a02 = A[u][2], a03 = A[u][3];
-                    const uint32_t a10 = A[u][4], a11 = A[u][5], a20 = A[u][6], a21 = A[u][7];
-                    const uint32_t a30 = A[u][8], a31 = A[u][9], a32 = A[u][10], a33 = A[u][11];
-                    // haarX / haarY (surfd.cu:1171-1182 via getSum)
-                    const int32_t wav1 = (int32_t)((a21 + a00 - a01 - a20) - (a31 + a10 - a11 - a30));
-                    const int32_t wav2 = (int32_t)((a31 + a02 - a01 - a32) - (a33 + a00 - a03 - a30));
-                    const float weight = s_lut[f2i_rz(rp + cp2)];
-                    const float dx = (weight * (float)wav2) * INV255;
-                    const float dy = (weight * (float)wav1) * INV255;
-                    float S[NS];
-                    if constexpr (!EXT) {
-                        S[0] = dx; S[1] = fminf(dx, 0.f);          // bins 1 | 0 by sign of dx
-                        S[2] = dy; S[3] = fminf(dy, 0.f);          // bins 3 | 2 by sign of dy
-                    } else {
-                        const float adx = fabsf(dx), ady = fabsf(dy);
-                        S[0] = dx;  S[1] = dy < 0.f ? dx : 0.f;    // bins 1 | 0 by sign of dy
-                        S[2] = adx; S[3] = dy < 0.f ? adx : 0.f;   // bins 3 | 2
-                        S[4] = dy;  S[5] = dx < 0.f ? dy : 0.f;    // bins 5 | 4 by sign of dx
-                        S[6] = ady; S[7] = dx < 0.f ? ady : 0.f;   // bins 7 | 6
-                    }
-                    const float w0 = 1.f - rf;
-#pragma unroll
-                    for (int R = 0; R < WSZ; R++) {
-                        const float rw = (R == ri) ? w0 : ((R == ri + 1) ? rf : 0.f);
-#pragma unroll
-                        for (int s = 0; s < NS; s++) acc[R][s] = fmaf(S[s], rw, acc[R][s]);
-                    }
+        } else {
+            // ---- generic (hs = 2 step + 1 at exact half-way scales): 12
+            // gathers per sample
+            for (int k = h; k < nv; k += rstep) {
+                if (col_on) {
+                    const int rb = (iy + (t0 + k - iradius) * step) * ip4;
+                    const int q0 = rb + dR0, q2 = rb + ip4, q3 = rb + dR3;
+                    accum(bld(rsrc, q0 + oA), bld(rsrc, q0 + oB), bld(rsrc, q0 + oC), bld(rsrc, q0 + oC + 4),
+                          bld(rsrc, rb + oA), bld(rsrc, rb + oB), bld(rsrc, q2 + oA), bld(rsrc, q2 + oB),
+                          bld(rsrc, q3 + oA), bld(rsrc, q3 + oB), bld(rsrc, q3 + oC), bld(rsrc, q3 + oC + 4),
+                          t0 + k);
                 }
             }
         }
