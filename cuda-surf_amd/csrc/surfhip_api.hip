@@ -62,7 +62,9 @@ struct surfhip_detector {
     int* cand_count = nullptr;
     uint32_t* scan_key = nullptr;       // NMS survivors awaiting interpolation
     uint32_t* scan_src = nullptr;
-    int* scan_count = nullptr;
+    int* item_count = nullptr;          // survivors per NMS scan item
+    int* item_off = nullptr;            // their exclusive prefix (+ total)
+    int nitems = 0;                     // scan items per frame
     int* offsets = nullptr;
     int* order = nullptr;               // per frame: keypoint indices in row order (describe schedule)
     int* status = nullptr;
@@ -372,7 +374,7 @@ static int derive(surfhip_detector* d)
 static void free_all(surfhip_detector* d)
 {
     void* ptrs[] = {d->d_oct, d->ii, d->resp, d->colsum, d->cand, d->keys, d->gscratch, d->cand_count,
-                    d->scan_key, d->scan_src, d->scan_count,
+                    d->scan_key, d->scan_src, d->item_count, d->item_off,
                     d->offsets, d->order, d->status, d->pts1, d->desc1, d->count1};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -415,6 +417,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
         e = hipMalloc((void**)&(ptr), (bytes));              \
         if (e != hipSuccess) goto fail;                      \
     } while (0)
+    make_plan(d->P, d->oct, d->plan);
     ALLOC(d->d_oct, sizeof(OctaveParams) * kMaxOct);
     ALLOC(d->ii, B * d->P.ii_stride * sizeof(int32_t));
     ALLOC(d->resp, B * d->tot_osize * sizeof(float));
@@ -422,9 +425,12 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     ALLOC(d->cand, B * d->cap * sizeof(surfhip_point));
     ALLOC(d->keys, B * d->cap * sizeof(uint32_t));
     ALLOC(d->cand_count, B * sizeof(int));
-    ALLOC(d->scan_key, B * d->cap * sizeof(uint32_t));
-    ALLOC(d->scan_src, B * d->cap * sizeof(uint32_t));
-    ALLOC(d->scan_count, B * sizeof(int));
+    d->nitems = d->plan.nms_start[kMaxOct] * 4;
+    ALLOC(d->scan_key, B * (size_t)d->nitems * kItemCap * sizeof(uint32_t));
+    ALLOC(d->scan_src, B * (size_t)d->nitems * kItemCap * sizeof(uint32_t));
+    ALLOC(d->item_count, B * (size_t)d->nitems * sizeof(int));
+    // prefix (nitems + 1) followed by the scan's per-chunk totals
+    ALLOC(d->item_off, (2 * B * (size_t)d->nitems + 64) * sizeof(int));
     ALLOC(d->offsets, (B + 1) * sizeof(int));
     ALLOC(d->order, B * (size_t)max_pts * sizeof(int));
     ALLOC(d->status, 16);
@@ -435,7 +441,6 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
 #undef ALLOC
     // zero once: integral pad columns and response pad columns are never
     // written by the kernels and never read by them either
-    make_plan(d->P, d->oct, d->plan);
     e = hipMemcpy(d->d_oct, d->oct, sizeof(OctaveParams) * kMaxOct, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemset(d->ii, 0, B * d->P.ii_stride * sizeof(int32_t));
     if (e == hipSuccess) e = hipMemset(d->resp, 0, B * d->tot_osize * sizeof(float));
@@ -514,14 +519,14 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
     hipStream_t s = d->stream;
     const bool prof = d->profiling;
     HIPCHK(hipMemsetAsync(d->cand_count, 0, sizeof(int) * nframes, s));
-    HIPCHK(hipMemsetAsync(d->scan_count, 0, sizeof(int) * nframes, s));
+    HIPCHK(hipMemsetAsync(d->item_count, 0, sizeof(int) * (size_t)nframes * d->nitems, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[0], s));
     HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[1], s));
     HIPCHK(launch_hessian(d->ii, d->resp, nframes, d->P, d->d_oct, d->oct, d->plan, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[2], s));
-    HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->scan_key, d->scan_src, d->scan_count,
-                      d->cap, d->cand, d->keys, d->cand_count, d->cap, d->status, d->offsets, s));
+    HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->scan_key, d->scan_src, d->item_count,
+                      d->item_off, d->cand, d->keys, d->cand_count, d->cap, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[3], s));
     HIPCHK(launch_sort(d->cand, d->keys, d->gscratch, d->cand_count, d->cap, nframes, points, d->max_pts,
                        counts, d->offsets, d->order, d->status, s));

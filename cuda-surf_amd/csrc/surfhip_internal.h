@@ -20,6 +20,7 @@ constexpr int kMaxScale = 8;
 constexpr int kSortCap = 16384;     // candidates per frame sorted in LDS
 constexpr int kBandRows = 32;       // integral-image band height
 constexpr int kScanRows = 16;       // NMS block rows per scan workgroup (4 per wave)
+constexpr int kItemCap = 64 * (kScanRows / 4);   // 2x2x2 blocks (= survivor slots) per scan item
 
 // Per-octave geometry and Hessian/NMS parameters, exactly as the reference
 // host code derives them (surf.cpp:240-292, surfd.cu:2844-2865, 3062-3076).
@@ -74,10 +75,12 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan);
 hipError_t launch_hessian(const int32_t* ii, float* resp, int nframes, const FrameParams& P,
                           const OctaveParams* d_oct, const OctaveParams* h_oct, const LaunchPlan& plan,
                           hipStream_t s);
+// NMS scan items: one wave's 64 block columns x kScanRows / 4 block rows;
+// each item owns kItemCap survivor slots (no atomics in the scan).
 hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,
                       const OctaveParams* d_oct, const LaunchPlan& plan, uint32_t* scan_key, uint32_t* scan_src,
-                      int* scan_count, int scap, surfhip_point* cand, uint32_t* keys, int* cand_count, int cap,
-                      int* status, int* scratch_off, hipStream_t s);
+                      int* item_count, int* item_off, surfhip_point* cand, uint32_t* keys, int* cand_count, int cap,
+                      hipStream_t s);
 hipError_t launch_sort(const surfhip_point* cand, const uint32_t* keys, uint64_t* gscratch,
                        int* cand_count, int cap, int nframes, surfhip_point* out, int max_pts,
                        int* out_count, int* offsets, int* order, int* status, hipStream_t s);

@@ -983,7 +983,7 @@ __device__ __forceinline__ int wave_append(bool ok, int* counter)
 __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, const FrameParams& P,
                                               const OctaveParams* __restrict__ oct, const LaunchPlan& plan,
                                               uint32_t* __restrict__ scan_key, uint32_t* __restrict__ scan_src,
-                                              int* __restrict__ scan_count, int scap, int f, int gb, int wv,
+                                              int* __restrict__ item_count, int nitems_frame, int f, int gb, int wv,
                                               float* sbest, uint32_t* sinfo)
 {
     constexpr int NU = kScanRows / 4;        // block rows per lane
@@ -1046,6 +1046,12 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
     if (ncand == 0) return;
     wave_sync();
     const int bx0 = (lb % nbx) * 64;
+    // survivors go to this wave item's own region (no atomics): kItemCap
+    // entries at item * kItemCap, the count in item_count[item]
+    const size_t item = ((size_t)f * nitems_frame + gb) * 4 + wv;
+    uint32_t* rkey = scan_key + item * kItemCap;
+    uint32_t* rsrc_ = scan_src + item * kItemCap;
+    int nsurv = 0;
     for (int c0 = 0; c0 < ncand; c0 += 64) {
         const int ci = c0 + (int)lane_id();
         bool ok = false;
@@ -1074,88 +1080,120 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
 #pragma unroll
             for (int t = 0; t < 19; t++) ok = ok && !(best < nb[t]);
         }
-        const int slot = wave_append(ok, &scan_count[f]);
-        if (ok && slot < scap) {
-            scan_key[(size_t)f * scap + slot] = ((uint32_t)o << 29) | ((uint32_t)z << 28) | ((uint32_t)y << 14) | (uint32_t)x;
-            scan_src[(size_t)f * scap + slot] = ((uint32_t)s << 28) | ((uint32_t)r << 14) | (uint32_t)c;
+        const unsigned long long mo = __ballot(ok);
+        if (ok) {
+            const int slot = nsurv + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mo >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((unsigned)mo, 0u));
+            rkey[slot] = ((uint32_t)o << 29) | ((uint32_t)z << 28) | ((uint32_t)y << 14) | (uint32_t)x;
+            rsrc_[slot] = ((uint32_t)s << 28) | ((uint32_t)r << 14) | (uint32_t)c;
         }
+        nsurv += (int)__popcll(mo);
     }
+    if (lane_id() == 0u && nsurv > 0) item_count[item] = nsurv;
     wave_sync();
 }
 
 __global__ __launch_bounds__(256) void k_nms_scan(const float* __restrict__ resp, FrameParams P,
                                                   const OctaveParams* __restrict__ oct, LaunchPlan plan,
                                                   uint32_t* __restrict__ scan_key, uint32_t* __restrict__ scan_src,
-                                                  int* __restrict__ scan_count, int scap, int nframes)
+                                                  int* __restrict__ item_count, int nframes)
 {
     __shared__ float sbest[4][64 * (kScanRows / 4)];
     __shared__ uint32_t sinfo[4][64 * (kScanRows / 4)];
     int f, gb;
     if (!xcd_frame_block(plan.nms_start[kMaxOct], nframes, f, gb)) return;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    nms_scan_item(resp, P, oct, plan, scan_key, scan_src, scan_count, scap, f, gb, wv, sbest[wv], sinfo[wv]);
+    nms_scan_item(resp, P, oct, plan, scan_key, scan_src, item_count, plan.nms_start[kMaxOct], f, gb, wv, sbest[wv],
+                  sinfo[wv]);
 }
 
-// Exclusive prefix of min(count[f], cap) over the frames (one workgroup).
-__global__ __launch_bounds__(1024) void k_prefix_clamped(const int* __restrict__ counts, int nframes, int cap,
-                                                         int* __restrict__ offsets)
+// Exclusive prefix of n ints (n up to ~2M): each workgroup scans 2048
+// elements (block_excl_scan) and records its total, one workgroup scans the
+// totals, then the block offsets are added.  out[n] = total.
+constexpr int kScanChunk = 2048;
+
+__global__ __launch_bounds__(256) void k_scan_local(const int* __restrict__ in, int n, int* __restrict__ out,
+                                                    int* __restrict__ bsum)
+{
+    __shared__ uint32_t lds4[4];
+    const int b0 = blockIdx.x * kScanChunk + threadIdx.x * 8;
+    uint32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = (b0 + k < n) ? (uint32_t)in[b0 + k] : 0u;
+    const uint32_t last = v[7];
+    block_excl_scan<8>(v, lds4);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+        if (b0 + k < n) out[b0 + k] = (int)v[k];
+    if (threadIdx.x == 255) bsum[blockIdx.x] = (int)(v[7] + last);
+}
+
+__global__ __launch_bounds__(1024) void k_scan_top(int* __restrict__ bsum, int nb, int* __restrict__ out, int n)
 {
     __shared__ int part[1024];
-    const int per = (nframes + 1023) / 1024;
+    const int per = (nb + 1023) / 1024;
     const int b = threadIdx.x * per;
     int sum = 0;
-    for (int i = 0; i < per; i++) if (b + i < nframes) sum += min(counts[b + i], cap);
+    for (int i = 0; i < per; i++) if (b + i < nb) sum += bsum[b + i];
     part[threadIdx.x] = sum;
     __syncthreads();
     if (threadIdx.x == 0) {
         int run = 0;
         for (int t = 0; t < 1024; t++) { const int v = part[t]; part[t] = run; run += v; }
-        offsets[nframes] = run;
+        out[n] = run;
     }
     __syncthreads();
     int run = part[threadIdx.x];
     for (int i = 0; i < per; i++)
-        if (b + i < nframes) { offsets[b + i] = run; run += min(counts[b + i], cap); }
+        if (b + i < nb) { const int v = bsum[b + i]; bsum[b + i] = run; run += v; }
+}
+
+__global__ __launch_bounds__(256) void k_scan_add(int* __restrict__ out, int n, const int* __restrict__ bsum)
+{
+    const int add = bsum[blockIdx.x];
+    const int b0 = blockIdx.x * kScanChunk;
+    for (int i = threadIdx.x; i < kScanChunk && b0 + i < n; i += 256) out[b0 + i] += add;
+}
+
+static void launch_excl_scan(const int* in, int n, int* out, int* bsum, hipStream_t s)
+{
+    const int nb = (n + kScanChunk - 1) / kScanChunk;
+    k_scan_local<<<nb, 256, 0, s>>>(in, n, out, bsum);
+    k_scan_top<<<1, 1024, 0, s>>>(bsum, nb, out, n);
+    k_scan_add<<<nb, 256, 0, s>>>(out, n, bsum);
 }
 
 constexpr int kFitGrid = 1024;
 
 // Pass 2: interpolation + makePoint, one lane per survivor of the whole batch
-// (grid-stride over the prefix of the frames' survivor counts), so no lane
-// idles on the ~99 % of blocks that fail the 3x3x3 test and no workgroup is
-// launched for empty space.
+// (grid-stride over the prefix of the scan items' survivor counts), so no
+// lane idles on the ~99 % of blocks that fail the 3x3x3 test and no
+// workgroup is launched for empty space.
 __global__ __launch_bounds__(256) void k_nms_fit(const int32_t* __restrict__ ii, const float* __restrict__ resp,
                                                  FrameParams P, const OctaveParams* __restrict__ oct,
                                                  const uint32_t* __restrict__ scan_key,
                                                  const uint32_t* __restrict__ scan_src,
-                                                 const int* __restrict__ scan_count, const int* __restrict__ soff,
-                                                 int scap, int nframes,
+                                                 const int* __restrict__ soff, int nitems, int items_per_frame,
                                                  surfhip_point* __restrict__ cand, uint32_t* __restrict__ keys,
-                                                 int* __restrict__ cand_count, int cap, int* status)
+                                                 int* __restrict__ cand_count, int cap)
 {
-    if (blockIdx.x == 0 && threadIdx.x < 64) {
-        for (int f = threadIdx.x; f < nframes; f += 64)
-            if (scan_count[f] > scap) atomicOr(status, 4);
-    }
-    const int total = soff[nframes];
+    const int total = soff[nitems];
     const int stride = kFitGrid * 256;
     for (int base = blockIdx.x * 256 + (threadIdx.x & ~63); base < total; base += stride) {
         const int t = base + (int)lane_id();
         const bool act = t < total;
         int f = 0;
-        if (act) {                                   // frame of survivor t
-            int lo = 0, hi = nframes;
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (soff[mid] <= t) lo = mid; else hi = mid;
-            }
-            f = lo;
-        }
         surfhip_point pt;
         bool ok = false;
         uint32_t key = 0;
         if (act) {
-            const size_t src_i = (size_t)f * scap + (t - soff[f]);
+            int lo = 0, hi = nitems;                     // scan item holding survivor t
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (soff[mid] <= t) lo = mid; else hi = mid;
+            }
+            f = lo / items_per_frame;
+            const size_t src_i = (size_t)lo * kItemCap + (t - soff[lo]);
             key = scan_key[src_i];
             const uint32_t src = scan_src[src_i];
             const int o = (int)(key >> 29);
@@ -1184,15 +1222,17 @@ __global__ __launch_bounds__(256) void k_nms_fit(const int32_t* __restrict__ ii,
 
 hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,
                       const OctaveParams* d_oct, const LaunchPlan& plan, uint32_t* scan_key, uint32_t* scan_src,
-                      int* scan_count, int scap, surfhip_point* cand, uint32_t* keys, int* cand_count, int cap,
-                      int* status, int* scratch_off, hipStream_t s)
+                      int* item_count, int* item_off, surfhip_point* cand, uint32_t* keys, int* cand_count, int cap,
+                      hipStream_t s)
 {
-    if (plan.nms_start[kMaxOct] == 0) return hipSuccess;
-    k_nms_scan<<<dim3(((nframes + 7) & ~7) * plan.nms_start[kMaxOct]), 256, 0, s>>>(resp, P, d_oct, plan, scan_key,
-                                                                                     scan_src, scan_count, scap, nframes);
-    k_prefix_clamped<<<1, 1024, 0, s>>>(scan_count, nframes, scap, scratch_off);
-    k_nms_fit<<<kFitGrid, 256, 0, s>>>(ii, resp, P, d_oct, scan_key, scan_src, scan_count, scratch_off, scap, nframes,
-                                       cand, keys, cand_count, cap, status);
+    const int per = plan.nms_start[kMaxOct];
+    if (per == 0) return hipSuccess;
+    k_nms_scan<<<dim3(((nframes + 7) & ~7) * per), 256, 0, s>>>(resp, P, d_oct, plan, scan_key, scan_src, item_count,
+                                                                 nframes);
+    const int nitems = nframes * per * 4;
+    launch_excl_scan(item_count, nitems, item_off, item_off + nitems + 1, s);
+    k_nms_fit<<<kFitGrid, 256, 0, s>>>(ii, resp, P, d_oct, scan_key, scan_src, item_off, nitems, per * 4, cand, keys,
+                                       cand_count, cap);
     return hipGetLastError();
 }
 
