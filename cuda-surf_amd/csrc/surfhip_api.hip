@@ -50,6 +50,7 @@ struct surfhip_detector {
     OctaveParams oct[kMaxOct]{};
     OctaveParams* d_oct = nullptr;      // device copy read by the fused launches
     LaunchPlan plan{};
+    FarPlan far{};
     int W = 0, H = 0, max_batch = 0, max_pts = 0, cap = 0;
     int nbands = 0, CW = 0;
     size_t tot_osize = 0;
@@ -417,7 +418,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
         e = hipMalloc((void**)&(ptr), (bytes));              \
         if (e != hipSuccess) goto fail;                      \
     } while (0)
-    make_plan(d->P, d->oct, d->plan);
+    make_plan(d->P, d->oct, d->plan, d->far);
     ALLOC(d->d_oct, sizeof(OctaveParams) * kMaxOct);
     ALLOC(d->ii, B * d->P.ii_stride * sizeof(int32_t));
     ALLOC(d->resp, B * d->tot_osize * sizeof(float));
@@ -506,7 +507,7 @@ int surfhip_run_integral(surfhip_detector* d, const uint8_t* frames, int nframes
 int surfhip_run_hessian(surfhip_detector* d, int nframes)
 {
     if (!d || nframes < 1 || nframes > d->max_batch) return SURFHIP_ERR_INVALID;
-    HIPCHK(launch_hessian(d->ii, d->resp, nframes, d->P, d->d_oct, d->oct, d->plan, d->stream));
+    HIPCHK(launch_hessian(d->ii, d->resp, nframes, d->P, d->d_oct, d->oct, d->plan, d->far, d->stream));
     return SURFHIP_OK;
 }
 
@@ -523,7 +524,7 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
     if (prof) HIPCHK(hipEventRecord(d->ev[0], s));
     HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[1], s));
-    HIPCHK(launch_hessian(d->ii, d->resp, nframes, d->P, d->d_oct, d->oct, d->plan, s));
+    HIPCHK(launch_hessian(d->ii, d->resp, nframes, d->P, d->d_oct, d->oct, d->plan, d->far, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[2], s));
     HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->scan_key, d->scan_src, d->item_count,
                       d->item_off, d->cand, d->keys, d->cand_count, d->cap, s));

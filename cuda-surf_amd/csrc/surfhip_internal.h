@@ -70,11 +70,29 @@ struct LaunchPlan {
     int o1_lds;                     // octave 1 on the LDS ring (k_hess_o1)
     int o1_nbx;
 };
-void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan);
+// Octaves >= 2 on the streaming-accumulation kernel (k_hess_far): per far
+// octave, the corner terms of every (scale, dxx/dyy/dxy) sum grouped by
+// corner row (dr) and bucketed by dr mod delta; see surfhip_kernels.hip.
+namespace farc {
+constexpr int MAXO = 3;             // far octaves on the kernel (2, 3, 4)
+constexpr int STRIP = 256;          // image columns per workgroup strip
+constexpr int R = 8;                // image rows per step (one wave each)
+constexpr int THREADS = 64 * R;
+constexpr int NA = 32;              // accumulator rows (sample rows in flight, a power of 2)
+}
+struct FarOct {
+    int o, d, nS, drmax, accoff;    // accoff: int offset of the [NA][9][nS] accumulators
+};
+struct FarPlan {
+    int nfar;                       // 0: no far kernel
+    int H, nstrips, nsteps, lds_bytes, acc_total;
+    FarOct oc[farc::MAXO];
+};
+void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, FarPlan& far);
 
 hipError_t launch_hessian(const int32_t* ii, float* resp, int nframes, const FrameParams& P,
                           const OctaveParams* d_oct, const OctaveParams* h_oct, const LaunchPlan& plan,
-                          hipStream_t s);
+                          const FarPlan& far, hipStream_t s);
 // NMS scan items: one wave's 64 block columns x kScanRows / 4 block rows;
 // each item owns kItemCap survivor slots (no atomics in the scan).
 hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,

@@ -18,6 +18,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "surfhip_internal.h"
 
 namespace surfhip {
@@ -41,6 +44,31 @@ __device__ __forceinline__ int f2i_rz(float v) { return (int)v; }
 __device__ __forceinline__ unsigned lane_id()
 {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+// Buffer (SRD) memory ops.  A raw buffer load past num_records returns 0 and
+// a store past it is dropped, so loads and stores at image edges need no
+// branch: a branch around a load makes hipcc wait for it (vmcnt(0)) right
+// there, which serialises a prefetch pipeline, and a store under a divergent
+// branch makes the outstanding-op count unknown, so the next counted wait
+// becomes vmcnt(0) too.  Descriptors are built from wave-uniform values only.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kOOB = 0x80000000u;          // byte offset past every buffer here
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, long long bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 buf_ld4(rsrc_t r, uint32_t off)
+{
+    const v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+// streaming store (nt): response planes are read back only by the NMS pass
+__device__ __forceinline__ void buf_st_nt(rsrc_t r, uint32_t off, float v)
+{
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 2);
 }
 
 // LDS visibility between the lanes of one wave
@@ -415,41 +443,60 @@ __device__ __forceinline__ void hess_pair(const lds_u64* Tl, int sb, float norm,
 #undef HI
 }
 
+// offa / offb: byte offsets of samples ixa / ixb in plane 0 of the octave
+// (kOOB past the grid: the store is dropped)
 template <int S, int M, int X2, int X3, int X4>
-__device__ __forceinline__ void hess_store(const lds_u64* Tl, int sb, const OctaveParams& q, float* row, int iy,
-                                           int ixa, int ixb)
+__device__ __forceinline__ void hess_store(const lds_u64* Tl, int sb, const OctaveParams& q, rsrc_t R, int iy,
+                                           int ixa, int ixb, uint32_t offa, uint32_t offb)
 {
     float ha, hb;
     hess_pair<M, X2, X3, X4>(Tl, sb, q.norm[S], ha, hb);
     const int b1 = q.b1[S];
-    const bool vy = iy >= b1 && iy < q.sh - b1;
-    float* pl = row + (size_t)S * q.osize;
-    // streaming stores: the planes are read back only by the NMS pass
-    if (ixa < q.sw) __builtin_nontemporal_store((vy && ixa >= b1 && ixa < q.sw - b1) ? ha : 0.f, pl + ixa);
-    if (ixb < q.sw) __builtin_nontemporal_store((vy && ixb >= b1 && ixb < q.sw - b1) ? hb : 0.f, pl + ixb);
+    const bool v = iy >= b1 && iy < q.sh - b1;
+    const uint32_t po = (uint32_t)(S * q.osize) * 4u;
+    buf_st_nt(R, offa + po, (v && ixa >= b1 && ixa < q.sw - b1) ? ha : 0.f);
+    buf_st_nt(R, offb + po, (v && ixb >= b1 && ixb < q.sw - b1) ? hb : 0.f);
 }
 
 // One fill item: image row gy, columns xs + 4a .. + 3 and the same + 128.
 struct RowItem { uint4 g0, g1; };
 
-__device__ __forceinline__ RowItem o0_load(const uint32_t* __restrict__ I, const FrameParams& P, int gy, int gx)
+// Rows outside the image read 0 (offset past the buffer; a negative row
+// wraps to a huge unsigned offset).  Columns < 0 or >= ip read the
+// neighbouring row: they feed only samples outside every scale's valid
+// window (x0 - 16 >= 2 and x0 + 17 <= W for every valid sample of lobes
+// 3..11), whose response is written as 0.
+__device__ __forceinline__ RowItem o0_load(rsrc_t I, int ip, int gy, int gx, bool ok = true)
 {
+    const uint32_t off = ok ? (uint32_t)(gy * ip + gx) * 4u : kOOB;
     RowItem v;
-    v.g0 = make_uint4(0u, 0u, 0u, 0u);
-    v.g1 = v.g0;
-    if (gy >= 0 && gy < P.iH) {
-        const uint32_t* row = I + (size_t)gy * P.ip;
-        if (gx >= 0 && gx < P.ip) v.g0 = *reinterpret_cast<const uint4*>(row + gx);
-        if (gx + 128 < P.ip) v.g1 = *reinterpret_cast<const uint4*>(row + gx + 128);
-    }
+    v.g0 = buf_ld4(I, off);
+    v.g1 = buf_ld4(I, off + 512u);
     return v;
+}
+
+// Two dwords from independent registers into one LDS pair slot.  As an asm
+// statement, so hipcc neither merges the pair writes of an item into a
+// ds_write_b128 (whose 4-register data tuple it would assemble with copies
+// placed at the loop back-edge, waiting there for the loads still in
+// flight) nor counts it: callers drain lgkmcnt before the barrier.
+__device__ __forceinline__ void lds_write2(uint32_t addr, uint32_t a, uint32_t b)
+{
+    asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" ::"v"(addr), "v"(a), "v"(b) : "memory");
 }
 
 __device__ __forceinline__ void o0_store(uint64_t* T, int gy, int a, const RowItem& v)
 {
-    uint64_t* dst = T + (gy & (o0::NRING - 1)) * o0::ROWQ + 2 * a;
-    *reinterpret_cast<uint4*>(dst) = make_uint4(v.g0.x, v.g1.x, v.g0.z, v.g1.z);            // even plane
-    *reinterpret_cast<uint4*>(dst + o0::NK) = make_uint4(v.g0.y, v.g1.y, v.g0.w, v.g1.w);   // odd plane
+    const uint32_t dst = (uint32_t)reinterpret_cast<uintptr_t>(T + (gy & (o0::NRING - 1)) * o0::ROWQ + 2 * a);
+    lds_write2(dst, v.g0.x, v.g1.x);                        // even plane, pairs 2a, 2a + 1
+    lds_write2(dst + 8u, v.g0.z, v.g1.z);
+    lds_write2(dst + 8u * o0::NK, v.g0.y, v.g1.y);          // odd plane
+    lds_write2(dst + 8u * o0::NK + 8u, v.g0.w, v.g1.w);
+}
+
+__device__ __forceinline__ void lds_drain()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 __global__ __launch_bounds__(o0::THREADS, 4) void k_hess_o0(const int32_t* __restrict__ ii, float* __restrict__ resp,
@@ -464,57 +511,62 @@ __global__ __launch_bounds__(o0::THREADS, 4) void k_hess_o0(const int32_t* __res
     if (f >= nframes) return;
     const int IX0 = bx * o0::TXS;
     const int xs = 2 * IX0 - 16;
-    const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
+    const rsrc_t I = make_rsrc(ii + (size_t)f * P.ii_stride, (long long)P.iH * P.ip * 4);
+    const int ip = P.ip;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     // item it of a 16-row chunk starting at image row y: row y + it / 40, group it % 40
     const int ra0 = tid / 40, ga0 = tid - ra0 * 40;                 // it = tid          (< 640)
     const int it1 = tid + o0::THREADS;                               // it = tid + 512    (< 640 for tid < 128)
-    const int ra1 = it1 / 40, ga1 = it1 - ra1 * 40;
     const bool has1 = it1 < o0::ITEMS;
+    const int ra1 = it1 / 40, ga1 = it1 - ra1 * 40;     // threads without a second item load past the buffer
     // ---- prologue: image rows -16 .. 31
     for (int y = -16; y < 32; y += o0::STEP) {
-        const RowItem v0 = o0_load(I, P, y + ra0, xs + 4 * ga0);
-        RowItem v1;
-        if (has1) v1 = o0_load(I, P, y + ra1, xs + 4 * ga1);
+        const RowItem v0 = o0_load(I, ip, y + ra0, xs + 4 * ga0);
+        const RowItem v1 = o0_load(I, ip, y + ra1, xs + 4 * ga1, has1);
         o0_store(T, y + ra0, ga0, v0);
         if (has1) o0_store(T, y + ra1, ga1, v1);
     }
+    lds_drain();
     __syncthreads();
     const lds_u64* Tl = (const lds_u64*)T + lane;
     const int ixa = IX0 + lane, ixb = ixa + 64;
-    float* F = resp + (size_t)f * P.resp_stride + q.ooff;
+    const rsrc_t R = make_rsrc(resp + (size_t)f * P.resp_stride + q.ooff, (P.resp_stride - q.ooff) * 4);
     const int nsteps = (q.sh + 7) >> 3;
     // Two-deep prefetch: the rows step s + 2 adds (16 s + 48 ..) are loaded
     // at the start of step s and written to the ring at the end of step s + 1,
     // so each load has two steps of compute to land.  The rows step s + 1
     // adds (16 s + 32 ..) go into the slots of rows 16 s - 32 .., last read
-    // in step s - 1.
+    // in step s - 1.  Every global load and store of the loop is issued
+    // unconditionally (past the buffer where nothing is there), so hipcc's
+    // count of outstanding ops is exact and the wait before the ring write
+    // leaves the younger loads in flight.
     RowItem pa0, pa1, pb0, pb1;
-    pa0 = o0_load(I, P, 32 + ra0, xs + 4 * ga0);
-    if (has1) pa1 = o0_load(I, P, 32 + ra1, xs + 4 * ga1);
+    pa0 = o0_load(I, ip, 32 + ra0, xs + 4 * ga0);
+    pa1 = o0_load(I, ip, 32 + ra1, xs + 4 * ga1, has1);
     auto step = [&](int s, RowItem& cur0, RowItem& cur1, RowItem& nxt0, RowItem& nxt1) {
         const int yl = 16 * s + 48;                 // rows loaded now, for step s + 2
-        if (s + 2 < nsteps) {
-            nxt0 = o0_load(I, P, yl + ra0, xs + 4 * ga0);
-            if (has1) nxt1 = o0_load(I, P, yl + ra1, xs + 4 * ga1);
-        }
+        nxt0 = o0_load(I, ip, yl + ra0, xs + 4 * ga0);
+        nxt1 = o0_load(I, ip, yl + ra1, xs + 4 * ga1, has1);
         const int iy = 8 * s + w;
-        if (iy < q.sh) {
+        {
             const int sb = (2 * iy - 16) & (o0::NRING - 1);
-            float* row = F + (size_t)iy * q.sp;
-            hess_store<0, 3, 1, 2, 3>(Tl, sb, q, row, iy, ixa, ixb);
-            hess_store<1, 5, 2, 4, 6>(Tl, sb, q, row, iy, ixa, ixb);
-            hess_store<2, 7, 3, 6, 9>(Tl, sb, q, row, iy, ixa, ixb);
-            hess_store<3, 9, 4, 8, 12>(Tl, sb, q, row, iy, ixa, ixb);
-            hess_store<4, 11, 5, 10, 15>(Tl, sb, q, row, iy, ixa, ixb);
+            const bool rowok = iy < q.sh;
+            const uint32_t offa = (rowok && ixa < q.sw) ? (uint32_t)(iy * q.sp + ixa) * 4u : kOOB;
+            const uint32_t offb = (rowok && ixb < q.sw) ? (uint32_t)(iy * q.sp + ixb) * 4u : kOOB;
+            hess_store<0, 3, 1, 2, 3>(Tl, sb, q, R, iy, ixa, ixb, offa, offb);
+            hess_store<1, 5, 2, 4, 6>(Tl, sb, q, R, iy, ixa, ixb, offa, offb);
+            hess_store<2, 7, 3, 6, 9>(Tl, sb, q, R, iy, ixa, ixb, offa, offb);
+            hess_store<3, 9, 4, 8, 12>(Tl, sb, q, R, iy, ixa, ixb, offa, offb);
+            hess_store<4, 11, 5, 10, 15>(Tl, sb, q, R, iy, ixa, ixb, offa, offb);
         }
         if (s + 1 < nsteps) {
             const int yw = 16 * s + 32;             // rows step s + 1 needs
             o0_store(T, yw + ra0, ga0, cur0);
             if (has1) o0_store(T, yw + ra1, ga1, cur1);
         }
+        lds_drain();
         __syncthreads();
     };
     for (int s = 0; s < nsteps; s += 2) {
@@ -575,12 +627,12 @@ __device__ __forceinline__ float hess1(const uint32_t* Tl, int sb, float norm)
     return (rr * (p - q2)) * norm;
 }
 
-__device__ __forceinline__ uint4 o1_load(const uint32_t* __restrict__ I, const FrameParams& P, int gy, int gx)
+// Rows outside the image read 0; columns < 0 or >= ip (the neighbouring row)
+// feed only samples outside every scale's valid window (x0 - 35 >= 1 and
+// x0 + 35 <= W for every valid octave-1 sample).
+__device__ __forceinline__ uint4 o1_load(rsrc_t I, int ip, int gy, int gx, bool ok = true)
 {
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (gy >= 0 && gy < P.iH && gx >= 0 && gx < P.ip)
-        v = *reinterpret_cast<const uint4*>(I + (size_t)gy * P.ip + gx);
-    return v;
+    return buf_ld4(I, ok ? (uint32_t)(gy * ip + gx) * 4u : kOOB);
 }
 
 __device__ __forceinline__ void o1_store(uint32_t* T, int gy, int a, uint4 v)
@@ -602,48 +654,47 @@ __global__ __launch_bounds__(o1::THREADS, 1) void k_hess_o1(const int32_t* __res
     if (f >= nframes) return;
     const int IX0 = bx * o1::TXS;
     const int xs = 4 * IX0 - 36;
-    const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
+    const rsrc_t I = make_rsrc(ii + (size_t)f * P.ii_stride, (long long)P.iH * P.ip * 4);
+    const int ip = P.ip;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ra0 = tid / o1::NK, ga0 = tid - ra0 * o1::NK;                 // item tid
     const int it1 = tid + o1::THREADS;                                      // item tid + 768
     const int ra1 = it1 / o1::NK, ga1 = it1 - ra1 * o1::NK;
-    const bool has1 = it1 < o1::ITEMS;
+    const bool has1 = it1 < o1::ITEMS;                  // threads without a second item load past the buffer
     // ---- prologue: image rows -34 .. 47 (step 0's window)
     for (int it = tid; it < 82 * o1::NK; it += o1::THREADS) {
         const int r = it / o1::NK, a = it - r * o1::NK;
-        o1_store(T, r - 34, a, o1_load(I, P, r - 34, xs + 4 * a));
+        o1_store(T, r - 34, a, o1_load(I, ip, r - 34, xs + 4 * a));
     }
     __syncthreads();
     const uint32_t* Tl = T + lane;
     const int ix = IX0 + lane;
-    float* F = resp + (size_t)f * P.resp_stride + q.ooff;
+    const rsrc_t R = make_rsrc(resp + (size_t)f * P.resp_stride + q.ooff, (P.resp_stride - q.ooff) * 4);
     const int nsteps = (q.sh + 3) >> 2;
     const int ur = w & 3, us = w >> 2;            // this wave's (sample row, scale) unit
     const int b1 = q.b1[us];
     const float norm = q.norm[us];
-    float* plane = F + (size_t)(q.init_scale + us) * q.osize;
+    const uint32_t pofs = (uint32_t)((q.init_scale + us) * q.osize) * 4u;
     // two-deep prefetch, as in k_hess_o0: rows 16 s + 64 .. (step s + 2) load
     // now and land in the ring at the end of step s + 1
     uint4 pa0 = make_uint4(0u, 0u, 0u, 0u), pa1 = pa0, pb0 = pa0, pb1 = pa0;
-    pa0 = o1_load(I, P, 48 + ra0, xs + 4 * ga0);
-    if (has1) pa1 = o1_load(I, P, 48 + ra1, xs + 4 * ga1);
+    pa0 = o1_load(I, ip, 48 + ra0, xs + 4 * ga0);
+    pa1 = o1_load(I, ip, 48 + ra1, xs + 4 * ga1, has1);
     auto step = [&](int s, uint4& cur0, uint4& cur1, uint4& nxt0, uint4& nxt1) {
         const int yl = 16 * s + 64;
-        if (s + 2 < nsteps) {
-            nxt0 = o1_load(I, P, yl + ra0, xs + 4 * ga0);
-            if (has1) nxt1 = o1_load(I, P, yl + ra1, xs + 4 * ga1);
-        }
+        nxt0 = o1_load(I, ip, yl + ra0, xs + 4 * ga0);
+        nxt1 = o1_load(I, ip, yl + ra1, xs + 4 * ga1, has1);
         const int iy = 4 * s + ur;
-        if (iy < q.sh) {
+        {
             const int sb = (4 * iy - 34 + 2 * o1::NRING) % o1::NRING;
             float h;
             if (us == 0) h = hess1<15, 7, 14, 21>(Tl, sb, norm);
             else if (us == 1) h = hess1<19, 9, 18, 27>(Tl, sb, norm);
             else h = hess1<23, 11, 22, 33>(Tl, sb, norm);
             const bool v = iy >= b1 && iy < q.sh - b1 && ix >= b1 && ix < q.sw - b1;
-            if (ix < q.sw) __builtin_nontemporal_store(v ? h : 0.f, plane + (size_t)iy * q.sp + ix);
+            buf_st_nt(R, (iy < q.sh && ix < q.sw) ? pofs + (uint32_t)(iy * q.sp + ix) * 4u : kOOB, v ? h : 0.f);
         }
         if (s + 1 < nsteps) {
             const int yw = 16 * s + 48;
@@ -684,9 +735,91 @@ static bool o0_lds_ok(const FrameParams& P, const OctaveParams& q)
     return true;
 }
 
-void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan)
+// The corner terms of the reference's getHessian (surfd.cu:353-366) for one
+// scale, as (dr, dc, weight, slot): slot 0 = dxx sum (outer box - 3 inner),
+// 1 = dyy, 2 = dxy (S1 + S2 - S3 - S4); I(dr, dc) = ii[y0 + dr][x0 + dc].
+struct HCorner { int dr, dc, w, slot; };
+static int hessian_corners(int M, int X2, int X3, int X4, HCorner* out)
+{
+    int n = 0;
+    auto box = [&](int x1, int y1, int x2, int y2, int w, int slot) {   // getSum, surfd.cu:334-343
+        out[n++] = {y1 + 1, x1 + 1, w, slot};
+        out[n++] = {y2, x2, w, slot};
+        out[n++] = {y2, x1 + 1, -w, slot};
+        out[n++] = {y1 + 1, x2, -w, slot};
+    };
+    box(M + X2, X3, -M - X2, -X3, 1, 0);
+    box(X2, X3, -X2, -X3, -3, 0);
+    box(X3, M + X2, -X3, -M - X2, 1, 1);
+    box(X3, X2, -X3, -X2, -3, 1);
+    box(X4, 0, 0, -X4, 1, 2);
+    box(0, X4, -X4, 0, 1, 2);
+    box(X4, X4, 0, 0, -1, 2);
+    box(0, 0, -X4, -X4, -1, 2);
+    return n;
+}
+
+// Far-octave plan: octaves 2.. of the default geometry (init lobe 3,
+// sampling 2: lobes 31/39/47, 63/79/95, 127/159/191, the variants compiled
+// into surfhip_far.inc) whose accumulators fit k_hess_far's LDS; any other
+// octave stays on k_hessian.
+static void make_far_plan(const FrameParams& P, const OctaveParams* oct, FarPlan& F)
+{
+    F = FarPlan{};
+    static const int lobes[3][3] = {{31, 39, 47}, {63, 79, 95}, {127, 159, 191}};
+    int nfar = 0, hmax = 0, na = 0;
+    for (int o = 2; o < P.noct && nfar < farc::MAXO; o++) {
+        const OctaveParams& q = oct[o];
+        bool ok = P.sampling == 2 && q.delta == (8 << nfar) && q.nscale == 3 && q.init_scale == 2;
+        for (int i = 0; ok && i < 3; i++)
+            ok = q.mask[i] == lobes[nfar][i] && q.x2[i] == q.mask[i] / 2 && q.x3[i] == 2 * (q.mask[i] / 2) &&
+                 q.x4[i] == 3 * (q.mask[i] / 2);
+        if (!ok) break;
+        int drmin = 1 << 30, drmax = -(1 << 30);
+        for (int i = 0; i < 3; i++) {
+            HCorner t[32];
+            const int k = hessian_corners(q.mask[i], q.x2[i], q.x3[i], q.x4[i], t);
+            for (int j = 0; j < k; j++) {
+                hmax = std::max(hmax, std::abs(t[j].dc));
+                drmin = std::min(drmin, t[j].dr);
+                drmax = std::max(drmax, t[j].dr);
+            }
+        }
+        FarOct& fo = F.oc[nfar];
+        fo.o = o;
+        fo.d = q.delta;
+        fo.nS = farc::STRIP / q.delta;
+        fo.drmax = drmax;
+        // sample rows in flight: a row's slot is reused NA rows later, which
+        // must start after the step that finalises it has ended
+        na = std::max(na, (drmax - drmin + farc::R - 1) / q.delta + 1);
+        nfar++;
+    }
+    if (nfar == 0) return;
+    if (na > farc::NA) return;
+    F.H = hmax <= 144 ? 144 : 288;                       // the two compiled halos
+    int acc = 0;
+    for (int i = 0; i < nfar; i++) {
+        F.oc[i].accoff = acc;
+        acc += farc::NA * 9 * F.oc[i].nS;
+    }
+    F.acc_total = acc;
+    const int PL = (farc::STRIP + 2 * F.H) / 8;
+    F.lds_bytes = (farc::R * 8 * PL + acc) * 4;
+    if (F.lds_bytes > 160 * 1024) return;
+    int last = 0;
+    for (int i = 0; i < nfar; i++)
+        last = std::max(last, F.oc[i].d * (oct[F.oc[i].o].sh - 1) + F.oc[i].drmax);
+    F.nsteps = (last + 1 + farc::R - 1) / farc::R;
+    F.nsteps += F.nsteps & 1;                            // the loop runs steps in pairs
+    F.nstrips = (P.W + 1 + farc::STRIP - 1) / farc::STRIP;
+    F.nfar = nfar;
+}
+
+void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, FarPlan& far)
 {
     int hb = 0, nb = 0;
+    make_far_plan(P, oct, far);
     plan.o0_lds = P.noct > 0 && o0_lds_ok(P, oct[0]);
     plan.o0_nbx = (oct[0].sw + o0::TXS - 1) / o0::TXS;     // strips per frame
     plan.o0_blocks = plan.o0_nbx;
@@ -698,7 +831,9 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan)
         if (o < P.noct) {
             const OctaveParams& q = oct[o];
             plan.hess_nbx[o] = (q.sw + 63) / 64;
-            if (!(o == 0 && plan.o0_lds) && !(o == 1 && plan.o1_lds)) hb += plan.hess_nbx[o] * ((q.sh + 3) / 4);
+            const bool on_far = o >= 2 && o < 2 + far.nfar;
+            if (!(o == 0 && plan.o0_lds) && !(o == 1 && plan.o1_lds) && !on_far)
+                hb += plan.hess_nbx[o] * ((q.sh + 3) / 4);
             plan.nms_nbx[o] = (q.nms_gx + 63) / 64;
             plan.nms_nby[o] = (q.nms_gy + kScanRows - 1) / kScanRows;
             nb += 2 * plan.nms_nbx[o] * plan.nms_nby[o];
@@ -759,15 +894,212 @@ __global__ __launch_bounds__(256) void k_hessian(const int32_t* __restrict__ ii,
     }
 }
 
+// ----------------------------------------------------------------------
+// Octaves >= 2 (delta 8, 16, 32): streaming accumulation.  A sample's 32
+// corners per scale span 142 (octave 2) to 574 (octave 4) image rows, more
+// than an LDS ring can hold, and gathering them per sample touches a cache
+// line per lane.  Instead a workgroup walks a 512-column strip of one frame
+// top to bottom, reading each integral row once (coalesced) into an LDS row
+// stored as 8 residue planes (column mod 8), and every corner on that row
+// adds its weighted value into the int32 sums (dxx, dyy, dxy per scale) of
+// its sample, kept in LDS.  The sums are exact mod 2^32 and order-free, i.e.
+// identical to the reference's int arithmetic (getHessian,
+// surfd.cu:353-366); a sample row is finalised (float math in the
+// reference's order, surfd.cu:480) once its last corner row has passed.
+// Row Y carries only the corner groups of class Y mod delta, unrolled per
+// class in surfhip_far.inc (tools/gen_far.py), so every corner read is an
+// LDS immediate offset from the lane's base.
+// Wave w takes row Y0 + w of each step (R = 8 rows) for every far octave
+// and finalises (octave, scale) units w and w + 8 (unit = 3 octave + scale).
+// The ring holds one step; its rows were loaded into registers two steps
+// earlier.  Small workgroups (256-column strips, ~50 KiB LDS) so that
+// several share a CU and overlap each other's barriers; the strips of a
+// frame run on one XCD, so the column halo comes from L2 (HBM reads = one
+// integral image per frame, FETCH_SIZE).
+// LDS: ring[R][8 planes][PL] | acc (per octave [NA][9][nS]).
+// ----------------------------------------------------------------------
+#include "surfhip_far.inc"
+
+template <int NI, int H>
+__device__ __forceinline__ void far_load(uint4 (&dst)[NI], rsrc_t I, int ip, int iH, int cs, int Y0)
+{
+    constexpr int NC4 = (farc::STRIP + 2 * H) / 4;
+#pragma unroll
+    for (int i = 0; i < NI; i++) {
+        const int t = (int)threadIdx.x + i * farc::THREADS;
+        const int r = t / NC4, q = t - r * NC4;
+        const int gy = Y0 + r;
+        const bool ok = r < farc::R && gy < iH;
+        dst[i] = buf_ld4(I, ok ? (uint32_t)(gy * ip + cs + 4 * q) * 4u : kOOB);
+    }
+}
+
+// columns 4q .. 4q + 3 of a row go to planes (4q & 7) + 0..3, index q / 2
+template <int NI, int H>
+__device__ __forceinline__ void far_ring_store(const uint4 (&src)[NI], uint32_t* ring)
+{
+    constexpr int NC4 = (farc::STRIP + 2 * H) / 4, PL = (farc::STRIP + 2 * H) / 8;
+#pragma unroll
+    for (int i = 0; i < NI; i++) {
+        const int t = (int)threadIdx.x + i * farc::THREADS;
+        const int r = t / NC4, q = t - r * NC4;
+        if (r < farc::R) {
+            uint32_t* d = ring + (r * 8 + 4 * (q & 1)) * PL + (q >> 1);
+            d[0] = src[i].x;
+            d[PL] = src[i].y;
+            d[2 * PL] = src[i].z;
+            d[3 * PL] = src[i].w;
+        }
+    }
+}
+
+template <int NI, int H>
+__global__ __launch_bounds__(farc::THREADS, 2) void k_hess_far(const int32_t* __restrict__ ii,
+                                                              float* __restrict__ resp, FrameParams P,
+                                                              const OctaveParams* __restrict__ oct, FarPlan F,
+                                                              int nframes)
+{
+    constexpr int PL = (farc::STRIP + 2 * H) / 8;
+    constexpr int ROWW = 8 * PL;
+    static_assert(farc::THREADS == 64 * farc::R, "one wave per ring row");
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    const int xcd = blockIdx.x & 7, kb = blockIdx.x >> 3;
+    const int f = (kb / F.nstrips) * 8 + xcd, strip = kb - (kb / F.nstrips) * F.nstrips;
+    if (f >= nframes) return;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int X0 = strip * farc::STRIP, cs = X0 - H;
+    const int nfar = F.nfar;
+    uint32_t* ring = sm;
+    int* acc = reinterpret_cast<int*>(sm + farc::R * ROWW);
+    for (int i = tid; i < F.acc_total; i += farc::THREADS) acc[i] = 0;
+    const rsrc_t I = make_rsrc(ii + (size_t)f * P.ii_stride, (long long)P.iH * P.ip * 4);
+    const rsrc_t Rs = make_rsrc(resp + (size_t)f * P.resp_stride, P.resp_stride * 4);
+    const int ip = P.ip, iH = P.iH;
+    const int sh2 = oct[2].sh;
+    const int sh3 = nfar > 1 ? oct[3].sh : 0, sh4 = nfar > 2 ? oct[4].sh : 0;
+    int next_iy[farc::MAXO] = {0, 0, 0};
+
+    uint4 A[NI], B[NI];
+    far_load<NI, H>(A, I, ip, iH, cs, 0);                         // rows of step 0
+    far_load<NI, H>(B, I, ip, iH, cs, farc::R);                   // rows of step 1
+    // finalised responses of the previous step, stored at the start of the
+    // next one: every step issues its two stores before its loads, with no
+    // branch around them, so hipcc's count of outstanding VMEM ops is exact
+    // and the ring write waits only for the loads of two steps back
+    uint32_t poff[2] = {kOOB, kOOB};
+    float ph[2] = {0.f, 0.f};
+
+    // One step: rows Y0 .. Y0 + 7.  `cur` (this step's rows, loaded two
+    // steps earlier) goes to the ring, then `cur` receives the loads for
+    // step s + 2.
+    auto step = [&](int sidx, uint4 (&cur)[NI]) {
+        const int Y0 = sidx * farc::R;
+        far_ring_store<NI, H>(cur, ring);
+        buf_st_nt(Rs, poff[0], ph[0]);
+        buf_st_nt(Rs, poff[1], ph[1]);
+        far_load<NI, H>(cur, I, ip, iH, cs, Y0 + 2 * farc::R);
+        __syncthreads();
+        // ---- accumulate every corner on row Y0 + wave
+        {
+            const int Y = Y0 + wv;
+            const uint32_t* row = ring + wv * ROWW;
+            if (lane < farc::STRIP / 8)
+                far_o2<H, PL>(Y & 7, row + lane, acc + F.oc[0].accoff + lane, Y >> 3, sh2);
+            if (nfar > 1 && lane < farc::STRIP / 16)
+                far_o3<H, PL>(Y & 15, row + 2 * lane, acc + F.oc[1].accoff + lane, Y >> 4, sh3);
+            if (nfar > 2 && lane < farc::STRIP / 32)
+                far_o4<H, PL>(Y & 31, row + 4 * lane, acc + F.oc[2].accoff + lane, Y >> 5, sh4);
+        }
+        __syncthreads();
+        // ---- finalise the sample row (of each far octave) whose last corner
+        // row has passed: at most one per octave per step (delta >= R); wave
+        // w takes units (octave, scale) w and w + 8
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const int unit = wv + farc::R * k;
+            const int fo_i = unit / 3, fo_s = unit - 3 * fo_i;
+            uint32_t off = kOOB;
+            float h = 0.f;
+            if (fo_i < nfar) {
+                const FarOct& fo = F.oc[fo_i];
+                const OctaveParams& q = oct[fo.o];
+                const int iy = next_iy[fo_i];
+                const int nS = fo.nS;
+                if (iy < q.sh && fo.d * iy + fo.drmax <= Y0 + farc::R - 1 && lane < nS) {
+                    const int ix = X0 / fo.d + lane;
+                    int* a = acc + fo.accoff + ((iy & (farc::NA - 1)) * 9 + 3 * fo_s) * nS + lane;
+                    const int32_t sxx = a[0], syy = a[nS], sxy = a[2 * nS];
+                    a[0] = 0;
+                    a[nS] = 0;
+                    a[2 * nS] = 0;
+                    const float rr = INV255 * INV255;
+                    const float dxx = (float)sxx;
+                    const float dyy = (float)syy;
+                    const float dxy = 0.6f * (float)sxy;
+                    const float pp = dxx * dyy;
+                    const float q2 = dxy * dxy;
+                    const int b1 = q.b1[fo_s];
+                    const bool v = iy >= b1 && iy < q.sh - b1 && ix >= b1 && ix < q.sw - b1;
+                    h = v ? (rr * (pp - q2)) * q.norm[fo_s] : 0.f;
+                    if (ix < q.sw)
+                        off = (uint32_t)(q.ooff + (long long)(q.init_scale + fo_s) * q.osize + (long long)iy * q.sp +
+                                         ix) * 4u;
+                }
+            }
+            poff[k] = off;
+            ph[k] = h;
+        }
+        // every wave tracks every octave's next row identically
+#pragma unroll
+        for (int oi = 0; oi < farc::MAXO; oi++) {
+            if (oi < nfar) {
+                const FarOct& fo = F.oc[oi];
+                if (next_iy[oi] < oct[fo.o].sh && fo.d * next_iy[oi] + fo.drmax <= Y0 + farc::R - 1) next_iy[oi]++;
+            }
+        }
+        __syncthreads();            // ring and finalised accumulators free for the next step
+    };
+    for (int s2 = 0; s2 < F.nsteps; s2 += 2) {
+        step(s2, A);
+        step(s2 + 1, B);
+    }
+    buf_st_nt(Rs, poff[0], ph[0]);
+    buf_st_nt(Rs, poff[1], ph[1]);
+}
+
+template <int NI, int H>
+static hipError_t launch_far(const int32_t* ii, float* resp, int nframes, const FrameParams& P,
+                             const OctaveParams* d_oct, const FarPlan& far, hipStream_t s)
+{
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_hess_far<NI, H>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const int nf8 = (nframes + 7) & ~7;
+    k_hess_far<NI, H><<<dim3(nf8 * far.nstrips), farc::THREADS, far.lds_bytes, s>>>(ii, resp, P, d_oct, far, nframes);
+    return hipSuccess;
+}
+
 hipError_t launch_hessian(const int32_t* ii, float* resp, int nframes, const FrameParams& P,
                           const OctaveParams* d_oct, const OctaveParams* h_oct, const LaunchPlan& plan,
-                          hipStream_t s)
+                          const FarPlan& far, hipStream_t s)
 {
     const int nf8 = (nframes + 7) & ~7;
     if (plan.o0_lds)
         k_hess_o0<<<dim3(nf8 * plan.o0_nbx), o0::THREADS, 0, s>>>(ii, resp, P, h_oct[0], plan.o0_nbx, nframes);
     if (plan.o1_lds)
         k_hess_o1<<<dim3(nf8 * plan.o1_nbx), o1::THREADS, 0, s>>>(ii, resp, P, h_oct[1], plan.o1_nbx, nframes);
+    if (far.nfar > 0) {
+        // rows of a step = R x (STRIP + 2H) columns in uint4 items: 1088 (H 144) / 1664 (H 288)
+        const hipError_t e = far.H == 144 ? launch_far<3, 144>(ii, resp, nframes, P, d_oct, far, s)
+                                          : launch_far<4, 288>(ii, resp, nframes, P, d_oct, far, s);
+        if (e != hipSuccess) return e;
+    }
     if (plan.hess_start[kMaxOct] > 0)
         k_hessian<<<dim3(nf8 * plan.hess_start[kMaxOct]), 256, 0, s>>>(ii, resp, P, d_oct, plan, nframes);
     return hipGetLastError();

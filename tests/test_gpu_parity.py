@@ -104,12 +104,15 @@ def _plane_views(resp, g, octs, p):
             yield o, s, resp[base:base + sh * sp].reshape(sh, sp)[:, :sw]
 
 
-@pytest.mark.parametrize("w,h", [(64, 48), (333, 211), (640, 480), (1920, 1080), (3840, 2160)])
-def test_hessian_planes_bit_exact(surf, orc, w, h):
+@pytest.mark.parametrize("w,h,noct", [(64, 48, 4), (333, 211, 4), (640, 480, 4), (1920, 1080, 4), (3840, 2160, 4),
+                                      (3840, 2160, 5), (1920, 1080, 6), (1100, 700, 5)])
+def test_hessian_planes_bit_exact(surf, orc, w, h, noct):
+    """Octaves 0/1 (LDS rings), 2-4 (streaming accumulation; 4 needs 5
+    octaves) and beyond (per-sample gather, the 6-octave case)."""
     frames = surf.synth_frames(1, w, h, first=7)
-    param = surf.make_param(4, 4.0, upright=True)
+    param = surf.make_param(noct, 4.0, upright=True)
     res = gpu_run(surf, param, frames, w, h, want_ws=True, desc=False)
-    op = orc.make_param(4, 4.0, upright=True)
+    op = orc.make_param(noct, 4.0, upright=True)
     _, ref, g, octs = orc.hessian(op, frames[0], w, h)
     got = res["resp"][0]
     for (o, s, rp), (_, _, gp) in zip(_plane_views(ref, g, octs, op), _plane_views(got, g, octs, op)):
