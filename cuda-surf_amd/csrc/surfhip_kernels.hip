@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "surfhip_internal.h"
 
@@ -54,6 +55,7 @@ __device__ __forceinline__ unsigned lane_id()
 // becomes vmcnt(0) too.  Descriptors are built from wave-uniform values only.
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
 constexpr uint32_t kOOB = 0x80000000u;          // byte offset past every buffer here
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* base, long long bytes)
@@ -2053,6 +2055,8 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
     __shared__ float s_cf[4][64];
     __shared__ float s_rf[4][64], s_rp[4][64];
     __shared__ int s_ri[4][64];
+    __shared__ float4 s_wr[4][64];               // per grid row: weights of cell rows 0..3
+    __shared__ __attribute__((aligned(16))) uint32_t s_seg[4][448];   // segment path: the wave's integral rows
     __shared__ unsigned long long s_mask[4][6];
     __shared__ float s_lut[40];
     if (threadIdx.x < 40) s_lut[threadIdx.x] = c_tab.lut2[threadIdx.x];
@@ -2107,7 +2111,6 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
         const int rlim = P.iH - 1 - hs, clim = P.W - hs;
         const int iradius = f2i_rn(((spacing * (float)(WSZ + 1)) * 0.5f) / (float)step);
         const int side = 2 * iradius + 1;
-        const bool dual = side <= 32;
         // ---- grid row t = lane: exact row geometry (surfd.cu:1290-1292)
         const int sit = lane - iradius;
         const float rpos_t = ((float)(step * sit) - dy0) / spacing;
@@ -2118,7 +2121,20 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
         s_rf[w][lane] = rx_t - (float)ri_t;
         s_rp[w][lane] = rpos_t * rpos_t;
         s_ri[w][lane] = ri_t;
-        // ---- grid column of this lane
+        {
+            // placeInIndex's row weights (surfd.cu:1199-1271): 1 - rfrac for
+            // cell row ri, rfrac for ri + 1
+            const float rf_t = rx_t - (float)ri_t, w0_t = 1.f - rf_t;
+            s_wr[w][lane] = make_float4(ri_t == 0 ? w0_t : (ri_t == -1 ? rf_t : 0.f),
+                                        ri_t == 1 ? w0_t : (ri_t == 0 ? rf_t : 0.f),
+                                        ri_t == 2 ? w0_t : (ri_t == 1 ? rf_t : 0.f),
+                                        ri_t == 3 ? w0_t : (ri_t == 2 ? rf_t : 0.f));
+        }
+        // ---- grid column of this lane (lane = j; dual: two half-waves of 32
+        // lanes walk alternate grid rows)
+        const int hmode = hs - 2 * step;          // 0 or -1: rows and columns share integral pairs
+        const bool share = hmode == 0 || hmode == -1;
+        const bool dual = side <= 32;
         const int j = dual ? (lane & 31) : lane;
         const int h = dual ? (lane >> 5) : 0;
         const int rstep = dual ? 2 : 1;
@@ -2141,8 +2157,7 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
 #pragma unroll
             for (int s = 0; s < NS; s++) acc[R][s] = 0.f;
         // ---- the valid grid rows form one contiguous run [t0, t0 + nv); half h
-        // takes rows t0 + h, t0 + h + rstep, ...  Rows go in batches of DU with
-        // all their loads issued first (the loop is latency-bound otherwise).
+        // takes rows t0 + h, t0 + h + rstep, ...
         // A row adds S * (1 - rfrac) to cell row ri and S * rfrac to ri + 1
         // (placeInIndex, surfd.cu:1199-1271); the weights of the 4 cell rows
         // are formed by selects, so the accumulators keep fixed registers.
@@ -2174,52 +2189,286 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
                 S[6] = ady; S[7] = dx < 0.f ? ady : 0.f;   // bins 7 | 6
             }
             const float w0 = 1.f - rf;
+            // the cell row is uniform over the wave except where the two
+            // halves (dual mode) straddle a cell-row boundary
+            const int riu = __builtin_amdgcn_readfirstlane(ri);
+            if (__all(ri == riu)) {
 #pragma unroll
-            for (int R = 0; R < WSZ; R++) {
-                const float rw = (R == ri) ? w0 : ((R == ri + 1) ? rf : 0.f);
+                for (int R = 0; R < WSZ; R++) {
+                    if (R == riu) {
 #pragma unroll
-                for (int s = 0; s < NS; s++) acc[R][s] = fmaf(S[s], rw, acc[R][s]);
-            }
-        };
-        const int hmode = hs - 2 * step;          // 0 or -1: the grid's rows share integral rows
-        if (hmode == 0 || hmode == -1) {
-            // ---- Row sharing.  step = rn(scale / 2) and hs = rz(scale) give
-            // hs = 2 step or 2 step - 1, so the outer rows r - hs and r + hs + 1
-            // of grid row i are rows r and r + 1 of grid rows i - 2 and i + 2.
-            // Each half walks every other grid row (dual: rows of its parity;
-            // single: even rows, then odd rows) keeping the (r, r + 1) rows of
-            // i - 2, i, i + 2 in registers: 8 loads per sample instead of 12.
-            const int nph = dual ? 1 : 2;
-            for (int ph = 0; ph < nph; ph++) {
-                const int hh = dual ? h : ph;
-                auto load8 = [&](int t, uint32_t (&T)[8]) {      // rows r, r+1 x cols c-s, c, c+1, c+s+1
-                    const int rb = (iy + (t - iradius) * step) * ip4, rb1 = rb + ip4;
-                    T[0] = bld(rsrc, rb + oA); T[1] = bld(rsrc, rb + oC); T[2] = bld(rsrc, rb + oC + 4);
-                    T[3] = bld(rsrc, rb + oB);
-                    T[4] = bld(rsrc, rb1 + oA); T[5] = bld(rsrc, rb1 + oC); T[6] = bld(rsrc, rb1 + oC + 4);
-                    T[7] = bld(rsrc, rb1 + oB);
-                };
-                uint32_t Pv[8], Cv[8], Nv[8];
-                const int tb = t0 + hh;
-                if (col_on && hh < nv) {
-                    load8(tb - 2, Pv);
-                    load8(tb, Cv);
-                }
-                for (int k = hh; k < nv; k += 2) {
-                    const int t = t0 + k;
-                    if (col_on) {
-                        load8(t + 2, Nv);
-                        const bool A = hmode == 0;
-                        // top row r - hs, bottom row r + hs + 1
-                        const uint32_t T0 = A ? Pv[0] : Pv[4], T1 = A ? Pv[1] : Pv[5];
-                        const uint32_t T2 = A ? Pv[2] : Pv[6], T3 = A ? Pv[3] : Pv[7];
-                        const uint32_t B0 = A ? Nv[4] : Nv[0], B1 = A ? Nv[5] : Nv[1];
-                        const uint32_t B2 = A ? Nv[6] : Nv[2], B3 = A ? Nv[7] : Nv[3];
-                        accum(T0, T3, T1, T2, Cv[0], Cv[3], Cv[4], Cv[7], B0, B3, B1, B2, t);
+                        for (int s = 0; s < NS; s++) acc[R][s] = fmaf(S[s], w0, acc[R][s]);
+                    } else if (R == riu + 1) {
 #pragma unroll
-                        for (int e = 0; e < 8; e++) { Pv[e] = Cv[e]; Cv[e] = Nv[e]; }
+                        for (int s = 0; s < NS; s++) acc[R][s] = fmaf(S[s], rf, acc[R][s]);
                     }
                 }
+            } else {
+#pragma unroll
+                for (int R = 0; R < WSZ; R++) {
+                    const float rw = (R == ri) ? w0 : ((R == ri + 1) ? rf : 0.f);
+#pragma unroll
+                    for (int s = 0; s < NS; s++) acc[R][s] = fmaf(S[s], rw, acc[R][s]);
+                }
+            }
+        };
+        if (share) {
+            // ---- Row and column sharing.  step = rn(scale / 2) and hs =
+            // rz(scale) give hs = 2 step or 2 step - 1, so the outer rows
+            // r - hs and r + hs + 1 of grid row i are rows r and r + 1 of grid
+            // rows i - 2 and i + 2, and likewise the columns.  Each half walks
+            // every other grid row (dual: rows of its parity; single: even
+            // rows, then odd rows).  Per integral row a lane loads its (c, c+1)
+            // pair (8 bytes, issued three grid rows ahead into a raw slot);
+            // when the row is first needed it takes columns c - hs and
+            // c + hs + 1 from lanes j -+ 2, except the two edge lanes on each
+            // side, which load that column themselves (the same instruction,
+            // every other lane past the buffer).  4 loads per sample (was 12).
+            const bool ld_on = j < side;
+            const bool eL = j < 2, eR = j + 2 >= side;
+            const int oE = eL ? oA : oB;          // edge lanes: c - hs (left) / c + hs + 1 (right)
+            const int nph = dual ? 1 : 2;
+            struct Raw { v2u32 lo, hi; uint32_t elo, ehi; };
+            auto ldraw = [&](int t) {
+                const int rb = (iy + (t - iradius) * step) * ip4;
+                const int o = ld_on ? rb + oC : (int)kOOB;
+                const int oe = (ld_on && (eL || eR)) ? rb + oE : (int)kOOB;
+                Raw q;
+#ifdef SURF_DIAG_NOLOAD
+                q.lo = v2u32{(uint32_t)o, (uint32_t)o + 7u};
+                q.hi = v2u32{(uint32_t)o * 3u, (uint32_t)o + 11u};
+                q.elo = (uint32_t)oe;
+                q.ehi = (uint32_t)oe * 5u;
+#elif defined(SURF_DIAG_NOEDGE)
+                q.lo = __builtin_amdgcn_raw_buffer_load_b64(rsrc, o, 0, 0);
+                q.hi = __builtin_amdgcn_raw_buffer_load_b64(rsrc, ld_on ? o + ip4 : (int)kOOB, 0, 0);
+                q.elo = (uint32_t)oe;
+                q.ehi = (uint32_t)oe * 5u;
+#else
+                q.lo = __builtin_amdgcn_raw_buffer_load_b64(rsrc, o, 0, 0);
+                q.hi = __builtin_amdgcn_raw_buffer_load_b64(rsrc, ld_on ? o + ip4 : (int)kOOB, 0, 0);
+                q.elo = bld(rsrc, oe);
+                q.ehi = bld(rsrc, (ld_on && (eL || eR)) ? oe + ip4 : (int)kOOB);
+#endif
+                return q;
+            };
+            // The row loop, specialised on hmode (A: hs = 2 step).  A row adds
+            // S (1 - rfrac) to cell row ri and S rfrac to ri + 1: the four
+            // row weights come precomputed per grid row (s_wr).
+            auto rows = [&](auto AC) {
+                constexpr bool A = decltype(AC)::value;
+                // T = rows r, r+1 x cols c-s, c, c+1, c+s+1
+                auto proc = [&](const Raw& q, uint32_t (&T)[8]) {
+                    T[1] = q.lo.x; T[2] = q.lo.y; T[5] = q.hi.x; T[6] = q.hi.y;
+                    const uint32_t l0 = (uint32_t)__shfl((int)(A ? q.lo.x : q.lo.y), lane - 2, 64);
+                    const uint32_t r0 = (uint32_t)__shfl((int)(A ? q.lo.y : q.lo.x), lane + 2, 64);
+                    const uint32_t l1 = (uint32_t)__shfl((int)(A ? q.hi.x : q.hi.y), lane - 2, 64);
+                    const uint32_t r1 = (uint32_t)__shfl((int)(A ? q.hi.y : q.hi.x), lane + 2, 64);
+                    T[0] = eL ? q.elo : l0;
+                    T[3] = eR ? q.elo : r0;
+                    T[4] = eL ? q.ehi : l1;
+                    T[7] = eR ? q.ehi : r1;
+                };
+                for (int ph = 0; ph < nph; ph++) {
+                    const int hh = dual ? h : ph;
+                    // rows t0 + hh, t0 + hh + 2, ...: nstep of them (the halves
+                    // of a dual wave may differ by one; the loop runs the larger)
+                    const int nstep = max(nv - hh + 1, 0) >> 1;
+                    const int nmax = dual ? max(nv + 1, 0) >> 1 : nstep;
+                    if (nmax == 0) continue;
+#ifdef SURF_DIAG_NOROWS
+                    continue;
+#endif
+                    // one sample of grid row t from the sets of rows t - 2, t, t + 2
+                    auto sample = [&](int n, const uint32_t (&Pv)[8], const uint32_t (&Cv)[8],
+                                      const uint32_t (&Nv)[8]) {
+                        const int t = t0 + hh + 2 * n;
+                        if (!(col_on && n < nstep)) return;
+#ifdef SURF_DIAG_NOCOMP
+                        acc[0][0] += (float)(Pv[0] ^ Cv[3] ^ Nv[5] ^ Pv[7] ^ Nv[1]);
+                        return;
+#endif
+                        const float rp = s_rp[w][t];
+                        const float4 wr = s_wr[w][t];
+                        // top row r - hs, bottom row r + hs + 1; rows r-s, r, r+1,
+                        // r+s+1 (a0*, a1*, a2*, a3*), cols c-s, c+s+1, c, c+1
+                        const uint32_t a00 = A ? Pv[0] : Pv[4], a02 = A ? Pv[1] : Pv[5];
+                        const uint32_t a03 = A ? Pv[2] : Pv[6], a01 = A ? Pv[3] : Pv[7];
+                        const uint32_t a30 = A ? Nv[4] : Nv[0], a32 = A ? Nv[5] : Nv[1];
+                        const uint32_t a33 = A ? Nv[6] : Nv[2], a31 = A ? Nv[7] : Nv[3];
+                        const uint32_t a10 = Cv[0], a11 = Cv[3], a20 = Cv[4], a21 = Cv[7];
+                        // haarX / haarY (surfd.cu:1171-1182 via getSum)
+                        const int32_t wav1 = (int32_t)((a21 + a00 - a01 - a20) - (a31 + a10 - a11 - a30));
+                        const int32_t wav2 = (int32_t)((a31 + a02 - a01 - a32) - (a33 + a00 - a03 - a30));
+                        const float weight = s_lut[f2i_rz(rp + cp2)];
+                        const float dx = (weight * (float)wav2) * INV255;
+                        const float dy = (weight * (float)wav1) * INV255;
+                        float S[NS];
+                        if constexpr (!EXT) {
+                            S[0] = dx; S[1] = fminf(dx, 0.f);          // bins 1 | 0 by sign of dx
+                            S[2] = dy; S[3] = fminf(dy, 0.f);          // bins 3 | 2 by sign of dy
+                        } else {
+                            const float adx = fabsf(dx), ady = fabsf(dy);
+                            S[0] = dx;  S[1] = dy < 0.f ? dx : 0.f;    // bins 1 | 0 by sign of dy
+                            S[2] = adx; S[3] = dy < 0.f ? adx : 0.f;   // bins 3 | 2
+                            S[4] = dy;  S[5] = dx < 0.f ? dy : 0.f;    // bins 5 | 4 by sign of dx
+                            S[6] = ady; S[7] = dx < 0.f ? ady : 0.f;   // bins 7 | 6
+                        }
+                        // all four cell rows with the row's weights (two are 0):
+                        // branch-free, fixed registers
+                        const float wrr[WSZ] = {wr.x, wr.y, wr.z, wr.w};
+#pragma unroll
+                        for (int R = 0; R < WSZ; R++)
+#pragma unroll
+                            for (int e = 0; e < NS; e++) acc[R][e] = fmaf(S[e], wrr[R], acc[R][e]);
+                    };
+                    // 8-value sets X, Y, Z rotate through the roles (top, middle,
+                    // bottom) and raw slots s0..s2 hold the rows 2, 4, 6 ahead;
+                    // unrolled by 3 so no register moves the sets around.  All
+                    // loads are unconditional (past the buffer where not needed),
+                    // so hipcc's outstanding-load count stays exact.
+                    uint32_t X[8], Y[8], Z[8];
+                    const int tb = t0 + hh;
+                    {
+                        const Raw q0 = ldraw(tb - 2), q1 = ldraw(tb);
+                        proc(q0, X);
+                        proc(q1, Y);
+                    }
+                    Raw s0 = ldraw(tb + 2), s1 = ldraw(tb + 4), s2 = ldraw(tb + 6);
+                    for (int n = 0; n < nmax; n += 3) {
+                        const int t = tb + 2 * n;
+                        proc(s0, Z);
+                        s0 = ldraw(t + 8);
+                        sample(n, X, Y, Z);
+                        proc(s1, X);
+                        s1 = ldraw(t + 10);
+                        sample(n + 1, Y, Z, X);
+                        proc(s2, Y);
+                        s2 = ldraw(t + 12);
+                        sample(n + 2, Z, X, Y);
+                    }
+                }
+            };
+            // ---- segment path (step <= 3, ~80 % of keypoints): the needed
+            // columns c_j - hs .. c_j + hs + 1 of all grid columns tile one
+            // contiguous span of each integral row, so a wave step loads the
+            // span of its 2 (dual: 4) integral rows as 16-byte chunks (1-2
+            // instructions instead of 4), stages them in a per-wave LDS row
+            // buffer and every lane reads its 8 values from there.
+            const int G = dual ? 2 : 1;
+            const int cs = (ix + (-2 - iradius) * step) & ~3;
+            const int W4 = (ix + (side + 1 - iradius) * step + 2 - cs + 3) >> 2;
+            const int WP = 4 * W4;
+            const int nitem = 2 * G * W4;
+            const bool seg = step <= 3 && nitem <= 128 && 2 * G * WP <= 448;
+            auto rows_seg = [&](auto AC) {
+                constexpr bool A = decltype(AC)::value;
+                uint32_t* buf = s_seg[w];
+                // chunk i of a wave step: integral row rr = 2 g + e of the step's
+                // grid rows, 16-byte chunk q; fixed per lane
+                int ckoff[2], cdst[2];
+                bool cok[2];
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+                    const int k = lane + 64 * i;
+                    const int rr = k / W4, q = k - rr * W4;
+                    cok[i] = k < nitem;
+                    cdst[i] = rr * WP + 4 * q;
+                    // integral row of grid row t0 (+ g): iy + (t0 + g - iradius) step + e
+                    ckoff[i] = ((iy + (t0 + (rr >> 1) - iradius) * step + (rr & 1)) * P.ip + cs + 4 * q) * 4;
+                }
+                const int gstride = 2 * step * ip4;             // two grid rows further down
+                struct Seg { uint4 c0, c1; };
+                auto ldseg = [&](int tt) {                      // grid rows t0 + tt (+ 1): tt relative
+                    Seg q;
+                    const int d = tt * step * ip4;
+                    q.c0 = buf_ld4(rsrc, cok[0] ? (uint32_t)(ckoff[0] + d) : kOOB);
+                    q.c1 = buf_ld4(rsrc, cok[1] ? (uint32_t)(ckoff[1] + d) : kOOB);
+                    return q;
+                };
+                const int xo = ld_on ? c - cs : 2 * hs;         // this lane's column in the buffer
+                const int rowg = (dual ? h : 0) * 2 * WP;
+                // T = rows r, r+1 x cols c-s, c, c+1, c+s+1
+                auto proc = [&](const Seg& q, uint32_t (&T)[8]) {
+                    if (cok[0]) *reinterpret_cast<uint4*>(buf + cdst[0]) = q.c0;
+                    if (cok[1]) *reinterpret_cast<uint4*>(buf + cdst[1]) = q.c1;
+                    wave_sync();
+                    const uint32_t* r0 = buf + rowg + xo;
+                    const uint32_t* r1 = r0 + WP;
+                    T[0] = r0[-hs]; T[1] = r0[0]; T[2] = r0[1]; T[3] = r0[hs + 1];
+                    T[4] = r1[-hs]; T[5] = r1[0]; T[6] = r1[1]; T[7] = r1[hs + 1];
+                    wave_sync();
+                };
+                (void)gstride;
+                for (int ph = 0; ph < (dual ? 1 : 2); ph++) {
+                    const int hh = dual ? h : ph;
+                    const int nstep = max(nv - hh + 1, 0) >> 1;
+                    const int nmax = dual ? max(nv + 1, 0) >> 1 : nstep;
+                    if (nmax == 0) continue;
+                    // grid-row offset of this phase's first row relative to t0
+                    // (dual: the chunks carry both halves' rows)
+                    const int pb = dual ? 0 : ph;
+                    auto sample = [&](int n, const uint32_t (&Pv)[8], const uint32_t (&Cv)[8],
+                                      const uint32_t (&Nv)[8]) {
+                        const int t = t0 + hh + 2 * n;
+                        if (!(col_on && n < nstep)) return;
+                        const float rp = s_rp[w][t];
+                        const float4 wr = s_wr[w][t];
+                        const uint32_t a00 = A ? Pv[0] : Pv[4], a02 = A ? Pv[1] : Pv[5];
+                        const uint32_t a03 = A ? Pv[2] : Pv[6], a01 = A ? Pv[3] : Pv[7];
+                        const uint32_t a30 = A ? Nv[4] : Nv[0], a32 = A ? Nv[5] : Nv[1];
+                        const uint32_t a33 = A ? Nv[6] : Nv[2], a31 = A ? Nv[7] : Nv[3];
+                        const uint32_t a10 = Cv[0], a11 = Cv[3], a20 = Cv[4], a21 = Cv[7];
+                        const int32_t wav1 = (int32_t)((a21 + a00 - a01 - a20) - (a31 + a10 - a11 - a30));
+                        const int32_t wav2 = (int32_t)((a31 + a02 - a01 - a32) - (a33 + a00 - a03 - a30));
+                        const float weight = s_lut[f2i_rz(rp + cp2)];
+                        const float dx = (weight * (float)wav2) * INV255;
+                        const float dy = (weight * (float)wav1) * INV255;
+                        float S[NS];
+                        if constexpr (!EXT) {
+                            S[0] = dx; S[1] = fminf(dx, 0.f);
+                            S[2] = dy; S[3] = fminf(dy, 0.f);
+                        } else {
+                            const float adx = fabsf(dx), ady = fabsf(dy);
+                            S[0] = dx;  S[1] = dy < 0.f ? dx : 0.f;
+                            S[2] = adx; S[3] = dy < 0.f ? adx : 0.f;
+                            S[4] = dy;  S[5] = dx < 0.f ? dy : 0.f;
+                            S[6] = ady; S[7] = dx < 0.f ? ady : 0.f;
+                        }
+                        const float wrr[WSZ] = {wr.x, wr.y, wr.z, wr.w};
+#pragma unroll
+                        for (int R = 0; R < WSZ; R++)
+#pragma unroll
+                            for (int e = 0; e < NS; e++) acc[R][e] = fmaf(S[e], wrr[R], acc[R][e]);
+                    };
+                    uint32_t X[8], Y[8], Z[8];
+                    {
+                        const Seg q0 = ldseg(pb - 2);
+                        proc(q0, X);
+                        const Seg q1 = ldseg(pb);
+                        proc(q1, Y);
+                    }
+                    Seg s0 = ldseg(pb + 2), s1 = ldseg(pb + 4), s2 = ldseg(pb + 6);
+                    for (int n = 0; n < nmax; n += 3) {
+                        const int tt = pb + 2 * n;
+                        proc(s0, Z);
+                        s0 = ldseg(tt + 8);
+                        sample(n, X, Y, Z);
+                        proc(s1, X);
+                        s1 = ldseg(tt + 10);
+                        sample(n + 1, Y, Z, X);
+                        proc(s2, Y);
+                        s2 = ldseg(tt + 12);
+                        sample(n + 2, Z, X, Y);
+                    }
+                }
+            };
+            if (seg) {
+                if (hmode == 0) rows_seg(std::integral_constant<bool, true>());
+                else rows_seg(std::integral_constant<bool, false>());
+            } else {
+                if (hmode == 0) rows(std::integral_constant<bool, true>());
+                else rows(std::integral_constant<bool, false>());
             }
         } else {
             // ---- generic (hs = 2 step + 1 at exact half-way scales): 12
@@ -2258,6 +2507,9 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
             const int col = R * NB + b;
             unsigned long long m0 = s_mask[w][C + 1], m1 = s_mask[w][C];
             float s = 0.f;
+#ifdef SURF_DIAG_NORED
+            m0 = 0; m1 = 0; s = red[w][lane][col];
+#endif
             while (m0) {
                 const int jj = __builtin_ctzll(m0);
                 m0 &= m0 - 1;
