@@ -103,6 +103,8 @@ def main():
     ap.add_argument("--pmc-json", default=None)
     ap.add_argument("--hessian-only", action="store_true",
                     help="time only the Hessian stage (for rocprofv3 --pmc passes)")
+    ap.add_argument("--with-integral", action="store_true",
+                    help="with --hessian-only: run the integral before every Hessian launch")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -140,6 +142,8 @@ def main():
 
     def run_batch():
         if args.hessian_only:
+            if args.with_integral:
+                det.run_integral(d_frames.data_ptr(), B, pitch, H * pitch)
             det.run_hessian(B)
         else:
             det.detect_batch(d_frames.data_ptr(), B, pitch, H * pitch, d_pts.data_ptr(), d_desc.data_ptr(),

@@ -77,6 +77,9 @@ struct surfhip_detector {
     hipEvent_t ev[SURFHIP_NSTAGE]{};
     float stage_ms[SURFHIP_NSTAGE]{};
     int last_nframes = 0;
+    const uint8_t* last_frames = nullptr;   // u8 source of the last integral (surfhip_run_hessian)
+    int last_pitch = 0;
+    long long last_fstride = 0;
     long long hess_bytes = 0;
 };
 
@@ -501,13 +504,17 @@ int surfhip_run_integral(surfhip_detector* d, const uint8_t* frames, int nframes
     int rc = check_frames(d, frames, nframes, pitch, stride);
     if (rc) return rc;
     HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, d->stream));
+    d->last_frames = frames;
+    d->last_pitch = pitch;
+    d->last_fstride = (long long)stride;
     return SURFHIP_OK;
 }
 
 int surfhip_run_hessian(surfhip_detector* d, int nframes)
 {
     if (!d || nframes < 1 || nframes > d->max_batch) return SURFHIP_ERR_INVALID;
-    HIPCHK(launch_hessian(d->ii, d->resp, nframes, d->P, d->d_oct, d->oct, d->plan, d->far, d->stream));
+    HIPCHK(launch_hessian(d->last_frames, d->last_pitch, d->last_fstride, d->ii, d->resp, nframes, d->P, d->d_oct,
+                          d->oct, d->plan, d->far, d->stream));
     return SURFHIP_OK;
 }
 
@@ -524,7 +531,8 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
     if (prof) HIPCHK(hipEventRecord(d->ev[0], s));
     HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[1], s));
-    HIPCHK(launch_hessian(d->ii, d->resp, nframes, d->P, d->d_oct, d->oct, d->plan, d->far, s));
+    HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
+                          d->plan, d->far, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[2], s));
     HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->scan_key, d->scan_src, d->item_count,
                       d->item_off, d->cand, d->keys, d->cand_count, d->cap, s));
@@ -536,6 +544,9 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
         HIPCHK(launch_describe(d->ii, d->P, points, d->max_pts, counts, d->offsets, d->order, nframes, desc, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[5], s));
     d->last_nframes = nframes;
+    d->last_frames = frames;
+    d->last_pitch = pitch;
+    d->last_fstride = (long long)stride;
     return SURFHIP_OK;
 }
 

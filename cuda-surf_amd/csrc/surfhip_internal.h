@@ -67,7 +67,9 @@ struct LaunchPlan {
     int nms_nbx[kMaxOct], nms_nby[kMaxOct];
     int o0_lds;                     // octave 0 on the LDS-tiled kernel (k_hess_o0)
     int o0_nbx, o0_blocks;
+    int o0_v, o0_vstrips;           // octave 0 on the u8 vertical-streaming kernel (k_hess_v0)
     int o1_lds;                     // octave 1 on the LDS ring (k_hess_o1)
+    int o1_v, o1_vstrips;           // octave 1 on the u8 vertical-streaming kernel (k_hess_v1)
     int o1_nbx;
 };
 // Octaves >= 2 on the streaming-accumulation kernel (k_hess_far): per far
@@ -90,9 +92,10 @@ struct FarPlan {
 };
 void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, FarPlan& far);
 
-hipError_t launch_hessian(const int32_t* ii, float* resp, int nframes, const FrameParams& P,
-                          const OctaveParams* d_oct, const OctaveParams* h_oct, const LaunchPlan& plan,
-                          const FarPlan& far, hipStream_t s);
+// frames may be null (no u8 source known): every octave then reads the integral image
+hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, const int32_t* ii, float* resp,
+                          int nframes, const FrameParams& P, const OctaveParams* d_oct, const OctaveParams* h_oct,
+                          const LaunchPlan& plan, const FarPlan& far, hipStream_t s);
 // NMS scan items: one wave's 64 block columns x kScanRows / 4 block rows;
 // each item owns kItemCap survivor slots (no atomics in the scan).
 hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,

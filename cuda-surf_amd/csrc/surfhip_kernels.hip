@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
+#include <utility>
 
 #include "surfhip_internal.h"
 
@@ -577,6 +578,9 @@ __global__ __launch_bounds__(o0::THREADS, 4) void k_hess_o0(const int32_t* __res
     }
 }
 
+#include "surfhip_hess_v0.inc"
+#include "surfhip_hess_v1.inc"
+
 // ----------------------------------------------------------------------
 // Octave 1 (4 px between samples, lobes 15/19/23: corner offsets -34..35):
 // the same strip walk with an LDS ring, one workgroup per CU.  A strip is
@@ -825,7 +829,11 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
     plan.o0_lds = P.noct > 0 && o0_lds_ok(P, oct[0]);
     plan.o0_nbx = (oct[0].sw + o0::TXS - 1) / o0::TXS;     // strips per frame
     plan.o0_blocks = plan.o0_nbx;
+    plan.o0_v = plan.o0_lds && getenv("SURFHIP_O0_RING") == nullptr;   // A/B switch back to k_hess_o0
+    plan.o0_vstrips = (oct[0].sw + 63) / 64;
     plan.o1_lds = P.noct > 1 && o1_lds_ok(P, oct[1]);
+    plan.o1_v = plan.o1_lds && getenv("SURFHIP_O1_RING") == nullptr;   // A/B switch back to k_hess_o1
+    plan.o1_vstrips = P.noct > 1 ? (oct[1].sw + 63) / 64 : 0;
     plan.o1_nbx = P.noct > 1 ? (oct[1].sw + o1::TXS - 1) / o1::TXS : 0;
     for (int o = 0; o < kMaxOct; o++) {
         plan.hess_start[o] = hb;
@@ -1087,14 +1095,22 @@ static hipError_t launch_far(const int32_t* ii, float* resp, int nframes, const 
     return hipSuccess;
 }
 
-hipError_t launch_hessian(const int32_t* ii, float* resp, int nframes, const FrameParams& P,
-                          const OctaveParams* d_oct, const OctaveParams* h_oct, const LaunchPlan& plan,
-                          const FarPlan& far, hipStream_t s)
+hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, const int32_t* ii, float* resp,
+                          int nframes, const FrameParams& P, const OctaveParams* d_oct, const OctaveParams* h_oct,
+                          const LaunchPlan& plan, const FarPlan& far, hipStream_t s)
 {
     const int nf8 = (nframes + 7) & ~7;
-    if (plan.o0_lds)
+    if (plan.o0_v && frames) {
+        const int per_xcd = (nf8 / 8) * plan.o0_vstrips;           // wave tasks per XCD
+        k_hess_v0<4, 1, 0x1f><<<dim3(8 * ((per_xcd + v0::WAVES - 1) / v0::WAVES)), v0::THREADS, 0, s>>>(
+            frames, pitch, fstride, resp, P, h_oct[0], plan.o0_vstrips, nframes);
+    } else if (plan.o0_lds)
         k_hess_o0<<<dim3(nf8 * plan.o0_nbx), o0::THREADS, 0, s>>>(ii, resp, P, h_oct[0], plan.o0_nbx, nframes);
-    if (plan.o1_lds)
+    if (plan.o1_v && frames) {
+        const int per_xcd = (nf8 / 8) * plan.o1_vstrips;
+        k_hess_v1<<<dim3(8 * ((per_xcd + v1::WAVES - 1) / v1::WAVES)), v1::THREADS, 0, s>>>(
+            frames, pitch, fstride, resp, P, h_oct[1], plan.o1_vstrips, nframes);
+    } else if (plan.o1_lds)
         k_hess_o1<<<dim3(nf8 * plan.o1_nbx), o1::THREADS, 0, s>>>(ii, resp, P, h_oct[1], plan.o1_nbx, nframes);
     if (far.nfar > 0) {
         // rows of a step = R x (STRIP + 2H) columns in uint4 items: 1088 (H 144) / 1664 (H 288)
