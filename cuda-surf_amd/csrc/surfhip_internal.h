@@ -70,6 +70,7 @@ struct LaunchPlan {
     int o0_v, o0_vstrips;           // octave 0 on the u8 vertical-streaming kernel (k_hess_v0)
     int o1_lds;                     // octave 1 on the LDS ring (k_hess_o1)
     int o1_v, o1_vstrips;           // octave 1 on the u8 vertical-streaming kernel (k_hess_v1)
+    int vfar_n;                     // octaves 2 .. 1 + vfar_n on k_hess_vfar (u8 vertical streaming)
     int o1_nbx;
 };
 // Octaves >= 2 on the streaming-accumulation kernel (k_hess_far): per far

@@ -580,6 +580,7 @@ __global__ __launch_bounds__(o0::THREADS, 4) void k_hess_o0(const int32_t* __res
 
 #include "surfhip_hess_v0.inc"
 #include "surfhip_hess_v1.inc"
+#include "surfhip_hess_vfar.inc"
 
 // ----------------------------------------------------------------------
 // Octave 1 (4 px between samples, lobes 15/19/23: corner offsets -34..35):
@@ -822,10 +823,29 @@ static void make_far_plan(const FrameParams& P, const OctaveParams* oct, FarPlan
     F.nfar = nfar;
 }
 
+// Octave o (2 or 3) of the default geometry (sampling 2: delta 8 / 16, lobes
+// 31/39/47, 63/79/95) goes to k_hess_vfar.
+static bool vfar_ok(const FrameParams& P, const OctaveParams& q, int o)
+{
+    const int d = 2 << o;
+    if (P.sampling != 2 || q.delta != d || q.nscale != 3 || q.init_scale != 2) return false;
+    for (int i = 0; i < 3; i++) {
+        const int X2 = (4 + i) * d / 2 - 1;
+        if (q.mask[i] != 2 * X2 + 1 || q.x2[i] != X2 || q.x3[i] != 2 * X2 || q.x4[i] != 3 * X2) return false;
+    }
+    return true;
+}
+
 void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, FarPlan& far)
 {
     int hb = 0, nb = 0;
-    make_far_plan(P, oct, far);
+    // k_hess_vfar (u8, 0.45 + 0.76 ms/batch for octaves 2 / 3) loses to the
+    // integral-image LDS kernel k_hess_far (1.03 ms for both) for now: opt-in
+    const bool use_vfar = getenv("SURFHIP_FAR_V") != nullptr;
+    plan.vfar_n = 0;
+    for (int o = 2; use_vfar && o < P.noct && o < 4 && vfar_ok(P, oct[o], o); o++) plan.vfar_n = o - 1;
+    if (plan.vfar_n > 0) far = FarPlan{};
+    else make_far_plan(P, oct, far);
     plan.o0_lds = P.noct > 0 && o0_lds_ok(P, oct[0]);
     plan.o0_nbx = (oct[0].sw + o0::TXS - 1) / o0::TXS;     // strips per frame
     plan.o0_blocks = plan.o0_nbx;
@@ -841,7 +861,7 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
         if (o < P.noct) {
             const OctaveParams& q = oct[o];
             plan.hess_nbx[o] = (q.sw + 63) / 64;
-            const bool on_far = o >= 2 && o < 2 + far.nfar;
+            const bool on_far = o >= 2 && o < 2 + (plan.vfar_n > 0 ? plan.vfar_n : far.nfar);
             if (!(o == 0 && plan.o0_lds) && !(o == 1 && plan.o1_lds) && !on_far)
                 hb += plan.hess_nbx[o] * ((q.sh + 3) / 4);
             plan.nms_nbx[o] = (q.nms_gx + 63) / 64;
@@ -1112,6 +1132,22 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
             frames, pitch, fstride, resp, P, h_oct[1], plan.o1_vstrips, nframes);
     } else if (plan.o1_lds)
         k_hess_o1<<<dim3(nf8 * plan.o1_nbx), o1::THREADS, 0, s>>>(ii, resp, P, h_oct[1], plan.o1_nbx, nframes);
+    if (plan.vfar_n > 0 && frames) {
+        // octave 2: 3 vertical segments, octave 3: 2 (parallelism); one launch each
+        for (int o = 2; o < 2 + plan.vfar_n; o++) {
+            const OctaveParams& q = h_oct[o];
+            const int nstrips = (q.sw + 63) / 64;
+            const int nseg = o == 2 ? 3 : 2;
+            const int segrows = (q.sh + nseg - 1) / nseg;
+            const int per_xcd = (nf8 / 8) * nstrips * nseg;
+            if (o == 2)
+                k_hess_vfar<8, 16, 8, 4, 4><<<dim3(8 * ((per_xcd + 3) / 4)), 256, 0, s>>>(
+                    frames, pitch, fstride, resp, P, q, nstrips, nseg, segrows, nframes);
+            else
+                k_hess_vfar<16, 32, 4, 4, 2><<<dim3(8 * ((per_xcd + 1) / 2)), 128, 0, s>>>(
+                    frames, pitch, fstride, resp, P, q, nstrips, nseg, segrows, nframes);
+        }
+    }
     if (far.nfar > 0) {
         // rows of a step = R x (STRIP + 2H) columns in uint4 items: 1088 (H 144) / 1664 (H 288)
         const hipError_t e = far.H == 144 ? launch_far<3, 144>(ii, resp, nframes, P, d_oct, far, s)
