@@ -75,6 +75,8 @@ struct surfhip_detector {
     int* count1 = nullptr;
     bool profiling = false;
     hipEvent_t ev[SURFHIP_NSTAGE]{};
+    hipStream_t side = nullptr;         // integral + integral-image Hessian kernels, beside the u8 ones
+    hipEvent_t fork = nullptr, join = nullptr;
     float stage_ms[SURFHIP_NSTAGE]{};
     int last_nframes = 0;
     const uint8_t* last_frames = nullptr;   // u8 source of the last integral (surfhip_run_hessian)
@@ -384,6 +386,9 @@ static void free_all(surfhip_detector* d)
         if (p) (void)hipFree(p);
     for (int i = 0; i < SURFHIP_NSTAGE; i++)
         if (d->ev[i]) (void)hipEventDestroy(d->ev[i]);
+    if (d->fork) (void)hipEventDestroy(d->fork);
+    if (d->join) (void)hipEventDestroy(d->join);
+    if (d->side) (void)hipStreamDestroy(d->side);
 }
 
 int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, int width, int height,
@@ -465,6 +470,10 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
         e = hipEventCreate(&d->ev[i]);
         if (e != hipSuccess) goto fail;
     }
+    e = hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&d->fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&d->join, hipEventDisableTiming);
+    if (e != hipSuccess) goto fail;
     *out = d;
     return SURFHIP_OK;
 fail:
@@ -528,12 +537,28 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
     const bool prof = d->profiling;
     HIPCHK(hipMemsetAsync(d->cand_count, 0, sizeof(int) * nframes, s));
     HIPCHK(hipMemsetAsync(d->item_count, 0, sizeof(int) * (size_t)nframes * d->nitems, s));
-    if (prof) HIPCHK(hipEventRecord(d->ev[0], s));
-    HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, s));
-    if (prof) HIPCHK(hipEventRecord(d->ev[1], s));
-    HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
-                          d->plan, d->far, s));
-    if (prof) HIPCHK(hipEventRecord(d->ev[2], s));
+    if (prof) {
+        // serial, so that the stage events bracket each stage alone
+        HIPCHK(hipEventRecord(d->ev[0], s));
+        HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, s));
+        HIPCHK(hipEventRecord(d->ev[1], s));
+        HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
+                              d->plan, d->far, s));
+        HIPCHK(hipEventRecord(d->ev[2], s));
+    } else {
+        // the u8 Hessian kernels (octaves 0, 1) need no integral image: they run
+        // on s beside the integral and the integral-image Hessian kernels
+        // (octaves >= 2) on the side stream; s waits for both
+        HIPCHK(hipEventRecord(d->fork, s));
+        HIPCHK(hipStreamWaitEvent(d->side, d->fork, 0));
+        HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, d->side));
+        HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
+                              d->plan, d->far, d->side, 2));
+        HIPCHK(hipEventRecord(d->join, d->side));
+        HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
+                              d->plan, d->far, s, 1));
+        HIPCHK(hipStreamWaitEvent(s, d->join, 0));
+    }
     HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->scan_key, d->scan_src, d->item_count,
                       d->item_off, d->cand, d->keys, d->cand_count, d->cap, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[3], s));

@@ -96,7 +96,7 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
 // frames may be null (no u8 source known): every octave then reads the integral image
 hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, const int32_t* ii, float* resp,
                           int nframes, const FrameParams& P, const OctaveParams* d_oct, const OctaveParams* h_oct,
-                          const LaunchPlan& plan, const FarPlan& far, hipStream_t s);
+                          const LaunchPlan& plan, const FarPlan& far, hipStream_t s, int parts = 3);
 // NMS scan items: one wave's 64 block columns x kScanRows / 4 block rows;
 // each item owns kItemCap survivor slots (no atomics in the scan).
 hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,

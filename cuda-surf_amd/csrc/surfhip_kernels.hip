@@ -1117,22 +1117,30 @@ static hipError_t launch_far(const int32_t* ii, float* resp, int nframes, const 
 
 hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, const int32_t* ii, float* resp,
                           int nframes, const FrameParams& P, const OctaveParams* d_oct, const OctaveParams* h_oct,
-                          const LaunchPlan& plan, const FarPlan& far, hipStream_t s)
+                          const LaunchPlan& plan, const FarPlan& far, hipStream_t s, int parts)
 {
     const int nf8 = (nframes + 7) & ~7;
+    // parts: 1 = the kernels that read the u8 frames, 2 = those that read the
+    // integral image (the two may run on different streams)
+    if (!frames) parts = 3;
+    const bool u8p = (parts & 1) != 0, iip = (parts & 2) != 0;
     if (plan.o0_v && frames) {
+        if (u8p) {
         const int per_xcd = (nf8 / 8) * plan.o0_vstrips;           // wave tasks per XCD
         k_hess_v0<4, 1, 0x1f><<<dim3(8 * ((per_xcd + v0::WAVES - 1) / v0::WAVES)), v0::THREADS, 0, s>>>(
             frames, pitch, fstride, resp, P, h_oct[0], plan.o0_vstrips, nframes);
-    } else if (plan.o0_lds)
+        }
+    } else if (plan.o0_lds && iip)
         k_hess_o0<<<dim3(nf8 * plan.o0_nbx), o0::THREADS, 0, s>>>(ii, resp, P, h_oct[0], plan.o0_nbx, nframes);
     if (plan.o1_v && frames) {
+        if (u8p) {
         const int per_xcd = (nf8 / 8) * plan.o1_vstrips;
         k_hess_v1<<<dim3(8 * ((per_xcd + v1::WAVES - 1) / v1::WAVES)), v1::THREADS, 0, s>>>(
             frames, pitch, fstride, resp, P, h_oct[1], plan.o1_vstrips, nframes);
-    } else if (plan.o1_lds)
+        }
+    } else if (plan.o1_lds && iip)
         k_hess_o1<<<dim3(nf8 * plan.o1_nbx), o1::THREADS, 0, s>>>(ii, resp, P, h_oct[1], plan.o1_nbx, nframes);
-    if (plan.vfar_n > 0 && frames) {
+    if (plan.vfar_n > 0 && frames && u8p) {
         // octave 2: 3 vertical segments, octave 3: 2 (parallelism); one launch each
         for (int o = 2; o < 2 + plan.vfar_n; o++) {
             const OctaveParams& q = h_oct[o];
@@ -1148,13 +1156,13 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
                     frames, pitch, fstride, resp, P, q, nstrips, nseg, segrows, nframes);
         }
     }
-    if (far.nfar > 0) {
+    if (far.nfar > 0 && iip) {
         // rows of a step = R x (STRIP + 2H) columns in uint4 items: 1088 (H 144) / 1664 (H 288)
         const hipError_t e = far.H == 144 ? launch_far<3, 144>(ii, resp, nframes, P, d_oct, far, s)
                                           : launch_far<4, 288>(ii, resp, nframes, P, d_oct, far, s);
         if (e != hipSuccess) return e;
     }
-    if (plan.hess_start[kMaxOct] > 0)
+    if (plan.hess_start[kMaxOct] > 0 && iip)
         k_hessian<<<dim3(nf8 * plan.hess_start[kMaxOct]), 256, 0, s>>>(ii, resp, P, d_oct, plan, nframes);
     return hipGetLastError();
 }
