@@ -1010,6 +1010,46 @@ __global__ __launch_bounds__(farc::THREADS, 2) void k_hess_far(const int32_t* __
     const int sh2 = oct[2].sh;
     const int sh3 = nfar > 1 ? oct[3].sh : 0, sh4 = nfar > 2 ? oct[4].sh : 0;
     int next_iy[farc::MAXO] = {0, 0, 0};
+    // the loop-invariant parameters of this wave's two finalisation units
+    // (octave, scale) = wv and wv + 8 and of the row tracking, read once
+    // (loads from oct inside the loop are repeated after every barrier)
+    struct FinUnit {
+        bool on, colok, colin;
+        int oi, d, drmax, nS, sh, sp, b1, accoff;
+        long long pbase;
+        float norm;
+    };
+    FinUnit fu[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int unit = wv + farc::R * k;
+        const int fo_i = unit / 3, fo_s = unit - 3 * fo_i;
+        FinUnit& u = fu[k];
+        u.on = fo_i < nfar;
+        const FarOct& fo = F.oc[u.on ? fo_i : 0];
+        const OctaveParams& q = oct[fo.o];
+        u.oi = u.on ? fo_i : 0;
+        u.d = fo.d;
+        u.drmax = fo.drmax;
+        u.nS = fo.nS;
+        u.sh = q.sh;
+        u.sp = q.sp;
+        u.b1 = q.b1[fo_s];
+        u.norm = q.norm[fo_s];
+        u.accoff = fo.accoff + 3 * fo_s * fo.nS + lane;
+        u.pbase = q.ooff + (long long)(q.init_scale + fo_s) * q.osize + X0 / fo.d + lane;
+        const int ix = X0 / fo.d + lane;
+        u.colok = ix >= u.b1 && ix < q.sw - u.b1;
+        u.colin = ix < q.sw;
+    }
+    int osh[farc::MAXO], odr[farc::MAXO], odm[farc::MAXO];
+#pragma unroll
+    for (int oi = 0; oi < farc::MAXO; oi++) {
+        const FarOct& fo = F.oc[oi < nfar ? oi : 0];
+        osh[oi] = oct[fo.o].sh;
+        odr[oi] = fo.d;
+        odm[oi] = fo.drmax;
+    }
 
     uint4 A[NI], B[NI];
     far_load<NI, H>(A, I, ip, iH, cs, 0);                         // rows of step 0
@@ -1031,16 +1071,13 @@ __global__ __launch_bounds__(farc::THREADS, 2) void k_hess_far(const int32_t* __
         buf_st_nt(Rs, poff[1], ph[1]);
         far_load<NI, H>(cur, I, ip, iH, cs, Y0 + 2 * farc::R);
         __syncthreads();
-        // ---- accumulate every corner on row Y0 + wave
+        // ---- accumulate every corner on the step's rows
         {
-            const int Y = Y0 + wv;
-            const uint32_t* row = ring + wv * ROWW;
-            if (lane < farc::STRIP / 8)
-                far_o2<H, PL>(Y & 7, row + lane, acc + F.oc[0].accoff + lane, Y >> 3, sh2);
-            if (nfar > 1 && lane < farc::STRIP / 16)
-                far_o3<H, PL>(Y & 15, row + 2 * lane, acc + F.oc[1].accoff + lane, Y >> 4, sh3);
-            if (nfar > 2 && lane < farc::STRIP / 32)
-                far_o4<H, PL>(Y & 31, row + 4 * lane, acc + F.oc[2].accoff + lane, Y >> 5, sh4);
+            // the step's corner groups of every far octave, dealt to the 8
+            // waves by cost (tools/gen_far.py, emit_balanced)
+            far_bal<H, PL, ROWW>(nfar, (Y0 >> 3) & 3, wv, ring, lane, acc + F.oc[0].accoff + lane,
+                                 acc + F.oc[1].accoff + lane, acc + F.oc[2].accoff + lane, Y0 >> 3, Y0 >> 4, Y0 >> 5,
+                                 sh2, sh3, sh4);
         }
         __syncthreads();
         // ---- finalise the sample row (of each far octave) whose last corner
@@ -1048,34 +1085,26 @@ __global__ __launch_bounds__(farc::THREADS, 2) void k_hess_far(const int32_t* __
         // w takes units (octave, scale) w and w + 8
 #pragma unroll
         for (int k = 0; k < 2; k++) {
-            const int unit = wv + farc::R * k;
-            const int fo_i = unit / 3, fo_s = unit - 3 * fo_i;
+            const FinUnit& u = fu[k];
             uint32_t off = kOOB;
             float h = 0.f;
-            if (fo_i < nfar) {
-                const FarOct& fo = F.oc[fo_i];
-                const OctaveParams& q = oct[fo.o];
-                const int iy = next_iy[fo_i];
-                const int nS = fo.nS;
-                if (iy < q.sh && fo.d * iy + fo.drmax <= Y0 + farc::R - 1 && lane < nS) {
-                    const int ix = X0 / fo.d + lane;
-                    int* a = acc + fo.accoff + ((iy & (farc::NA - 1)) * 9 + 3 * fo_s) * nS + lane;
-                    const int32_t sxx = a[0], syy = a[nS], sxy = a[2 * nS];
+            if (u.on) {
+                const int iy = next_iy[u.oi];
+                if (iy < u.sh && u.d * iy + u.drmax <= Y0 + farc::R - 1 && lane < u.nS) {
+                    int* a = acc + u.accoff + (iy & (farc::NA - 1)) * 9 * u.nS;
+                    const int32_t sxx = a[0], syy = a[u.nS], sxy = a[2 * u.nS];
                     a[0] = 0;
-                    a[nS] = 0;
-                    a[2 * nS] = 0;
+                    a[u.nS] = 0;
+                    a[2 * u.nS] = 0;
                     const float rr = INV255 * INV255;
                     const float dxx = (float)sxx;
                     const float dyy = (float)syy;
                     const float dxy = 0.6f * (float)sxy;
                     const float pp = dxx * dyy;
                     const float q2 = dxy * dxy;
-                    const int b1 = q.b1[fo_s];
-                    const bool v = iy >= b1 && iy < q.sh - b1 && ix >= b1 && ix < q.sw - b1;
-                    h = v ? (rr * (pp - q2)) * q.norm[fo_s] : 0.f;
-                    if (ix < q.sw)
-                        off = (uint32_t)(q.ooff + (long long)(q.init_scale + fo_s) * q.osize + (long long)iy * q.sp +
-                                         ix) * 4u;
+                    const bool v = iy >= u.b1 && iy < u.sh - u.b1 && u.colok;
+                    h = v ? (rr * (pp - q2)) * u.norm : 0.f;
+                    if (u.colin) off = (uint32_t)(u.pbase + iy * u.sp) * 4u;
                 }
             }
             poff[k] = off;
@@ -1084,12 +1113,11 @@ __global__ __launch_bounds__(farc::THREADS, 2) void k_hess_far(const int32_t* __
         // every wave tracks every octave's next row identically
 #pragma unroll
         for (int oi = 0; oi < farc::MAXO; oi++) {
-            if (oi < nfar) {
-                const FarOct& fo = F.oc[oi];
-                if (next_iy[oi] < oct[fo.o].sh && fo.d * next_iy[oi] + fo.drmax <= Y0 + farc::R - 1) next_iy[oi]++;
-            }
+            if (oi < nfar && next_iy[oi] < osh[oi] && odr[oi] * next_iy[oi] + odm[oi] <= Y0 + farc::R - 1) next_iy[oi]++;
         }
-        __syncthreads();            // ring and finalised accumulators free for the next step
+        // no barrier here: the next step's ring writes come after every wave
+        // passed this step's second barrier (all reads of the ring done), and
+        // the accumulator slots zeroed above are not reused for NA rows
     };
     for (int s2 = 0; s2 < F.nsteps; s2 += 2) {
         step(s2, A);
