@@ -120,6 +120,24 @@ def test_hessian_planes_bit_exact(surf, orc, w, h, noct):
         assert same.all(), f"octave {o} scale {s}: {(~same).sum()} cells differ, first at {np.argwhere(~same)[0]}"
 
 
+@pytest.mark.parametrize("env", ["SURFHIP_O0_RING", "SURFHIP_O1_RING", "SURFHIP_FAR_V"])
+@pytest.mark.parametrize("w,h,noct", [(640, 480, 4), (1920, 1080, 4)])
+def test_hessian_alternate_kernels_bit_exact(surf, orc, monkeypatch, env, w, h, noct):
+    """The selectable Hessian kernels (integral-image rings for octaves 0/1,
+    the u8 vertical-streaming kernel for octaves 2/3) give the same planes;
+    the plan reads these switches when a detector is created."""
+    monkeypatch.setenv(env, "1")
+    frames = surf.synth_frames(1, w, h, first=21)
+    param = surf.make_param(noct, 4.0, upright=True)
+    res = gpu_run(surf, param, frames, w, h, want_ws=True, desc=False)
+    op = orc.make_param(noct, 4.0, upright=True)
+    _, ref, g, octs = orc.hessian(op, frames[0], w, h)
+    got = res["resp"][0]
+    for (o, s, rp), (_, _, gp) in zip(_plane_views(ref, g, octs, op), _plane_views(got, g, octs, op)):
+        same = rp.view(np.uint32) == gp.view(np.uint32)
+        assert same.all(), f"{env}: octave {o} scale {s}: {(~same).sum()} cells differ"
+
+
 @pytest.mark.parametrize("upright,extend", [(True, False), (False, False), (True, True), (False, True)])
 def test_detect_describe_synthetic(surf, orc, upright, extend):
     w, h = 640, 480
