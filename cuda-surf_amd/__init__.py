@@ -114,6 +114,8 @@ _sigs = {
     "surfhip_slab_bytes": (_sz, [_i, _i, _i]),
     "surfhip_batch_total": (_i, [_vp, _i, C.POINTER(_i)]),
     "surfhip_pack_slab": (_i, [_vp, _vp, _vp, _vp, _i, _vp]),
+    "surfhip_match_scratch": (_sz, [_i, _i, _i]),
+    "surfhip_match": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp]),
     "surfhip_build_info": (C.c_char_p, []),
 }
 for _name, (_res, _args) in _sigs.items():
@@ -390,6 +392,34 @@ class Surfor:
             for name in POINT_DTYPE.names[:nf]:
                 result.h_data[name][:n] = tmp[name]
         return dptr if desc else None
+
+
+    def match(self, data1: SurfData, data2: SurfData, features1: int, features2: int) -> None:
+        """Surfor::match (surf.cpp:418-428): findMaxCorr of data1 against
+        data2 on the device, then the five match fields (score, match,
+        match_x, match_y, ambiguity) copied to data1.h_data."""
+        match_points(data1.d_data.ptr, data2.d_data.ptr, features1, features2, data1.num_pts,
+                     data2.num_pts, self.its.nfeatures)
+        synchronize()
+        if data1.h_data is not None and data1.num_pts > 0:
+            tmp = download_ptr(data1.d_data.ptr, POINT_DTYPE, data1.num_pts)
+            for name in ("score", "match", "match_x", "match_y", "ambiguity"):
+                data1.h_data[name][:data1.num_pts] = tmp[name]
+
+
+MATCH_FULL_TAIL = 1
+
+
+def match_points(pts1_ptr: int, pts2_ptr: int, feat1_ptr: int, feat2_ptr: int, n1: int, n2: int,
+                 nfeatures: int, flags: int = 0, scratch_ptr: int | None = None, stream=None) -> None:
+    """surfhip_match (cuFindMaxCorr, surfd.cu:3554-3566), asynchronous on
+    `stream` (a raw hipStream_t or None for the null stream)."""
+    check(_lib.surfhip_match(pts1_ptr, pts2_ptr, feat1_ptr, feat2_ptr, n1, n2, nfeatures, flags,
+                             scratch_ptr, stream), "surfhip_match")
+
+
+def match_scratch_bytes(n1: int, n2: int, flags: int = 0) -> int:
+    return int(_lib.surfhip_match_scratch(n1, n2, flags))
 
 
 # ---------------------------------------------------------------- frames

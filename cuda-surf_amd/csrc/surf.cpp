@@ -106,12 +106,17 @@ namespace surf
 
     void Surfor::match(SurfData& data1, SurfData& data2, float* features1, float* features2)
     {
-        (void)data1;
-        (void)data2;
-        (void)features1;
-        (void)features2;
-        fprintf(stderr, "Surfor::match: descriptor matching is not part of this engine's detect+describe path "
-                        "(SURVEY.md 8f).\n");
-        exit(-1);
+        // surf.cpp:418-428: cuFindMaxCorr on the device (synchronous, as the
+        // reference's cudaDeviceSynchronize), then score, match, match_x,
+        // match_y, ambiguity (5 consecutive 4-B fields at offset 28) to h_data.
+        CHECK(surfhip_match(reinterpret_cast<surfhip_point*>(data1.d_data),
+                            reinterpret_cast<const surfhip_point*>(data2.d_data), features1, features2,
+                            data1.num_pts, data2.num_pts, its.nfeatures, 0, nullptr, nullptr));
+        CHECK(surfhip_device_synchronize());
+        if (data1.h_data != NULL && data1.d_data != NULL && data1.num_pts > 0)
+        {
+            CHECK(surfhip_memcpy2d(&data1.h_data[0].score, sizeof(SurfPoint), &data1.d_data[0].score,
+                                   sizeof(SurfPoint), 5 * sizeof(float), (size_t)data1.num_pts, SURFHIP_D2H));
+        }
     }
 }

@@ -679,6 +679,36 @@ int surfhip_pack_slab(surfhip_detector* d, const surfhip_point* pts, const float
     return SURFHIP_OK;
 }
 
+size_t surfhip_match_scratch(int n1, int n2, int flags)
+{
+    if (n1 < 0 || n2 < 0) return 0;
+    return match_scratch_bytes(n1, n2, flags);
+}
+
+int surfhip_match(surfhip_point* pts1, const surfhip_point* pts2, const float* f1, const float* f2, int n1, int n2,
+                  int nf, int flags, void* scratch, void* stream)
+{
+    if (n1 < 0 || n2 < 0 || nf < 4 || nf > 128 || (nf & 3) || (flags & ~SURFHIP_MATCH_FULL_TAIL))
+        return SURFHIP_ERR_INVALID;
+    if (n1 == 0) return SURFHIP_OK;
+    if (!pts1 || !f1 || (n2 > 0 && (!pts2 || !f2))) return SURFHIP_ERR_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    const size_t bytes = match_scratch_bytes(n1, n2, flags);
+    void* own = nullptr;
+    if (!scratch && bytes) {            // no caller scratch: allocate, and finish before freeing it
+        HIPCHK(hipMalloc(&own, bytes));
+        scratch = own;
+    }
+    hipError_t e = launch_match(pts1, pts2, f1, f2, n1, n2, nf, flags, scratch, s);
+    if (own) {
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        hipError_t e2 = hipFree(own);
+        if (e == hipSuccess) e = e2;
+    }
+    HIPCHK(e);
+    return SURFHIP_OK;
+}
+
 const char* surfhip_build_info(void)
 {
     return "libsurfhip gfx950 (" __DATE__ " " __TIME__ ")";

@@ -109,6 +109,10 @@ hipError_t launch_sort(const surfhip_point* cand, const uint32_t* keys, uint64_t
 hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
                            const int* counts, const int* offsets, const int* order, int nframes, float* desc,
                            hipStream_t s);
+// Descriptor matching (surfhip_match.hip): scratch = match_scratch_bytes().
+size_t match_scratch_bytes(int n1, int n2, int flags);
+hipError_t launch_match(surfhip_point* pts1, const surfhip_point* pts2, const float* f1, const float* f2, int n1,
+                        int n2, int nf, int flags, void* scratch, hipStream_t s);
 hipError_t launch_pack(const surfhip_point* pts, const float* desc, const int* counts, const int* offsets,
                        int nframes, int max_pts, int nfeat, uint8_t* slab, hipStream_t s);
 

@@ -35,8 +35,9 @@ namespace surf
         void detectAndCompute(unsigned char* image, SurfData& result, int3 whp0, float** desc_addr,
                               const bool desc = true);
 
-        /* Descriptor matching (reference surf.cpp:418-428): not implemented
-         * by this engine yet; reports and exits. */
+        /* Descriptor matching (reference surf.cpp:418-428): for each point of
+         * data1 the best (score, match, match_x, match_y, ambiguity) over
+         * data2 on the device (surfhip_match), copied to data1.h_data. */
         void match(SurfData& data1, SurfData& data2, float* features1, float* features2);
 
     private:

@@ -185,6 +185,26 @@ int surfhip_batch_total(surfhip_detector* det, int nframes, int* total);
 int surfhip_pack_slab(surfhip_detector* det, const surfhip_point* d_points, const float* d_desc,
                       const int* d_counts, int nframes, void* d_slab);
 
+/* ------------------------------------------------------------ matching --
+ * Surfor::match (surf.cpp:418-428) -> cuFindMaxCorr (surfd.cu:3554-3566) ->
+ * findMaxCorr (surfd.cu:2530-2656), asynchronous on `stream` (NULL = the
+ * null stream).  For each of the n1 points of set 1 writes score (best dot
+ * product), match (index into set 2, -1 when no score is positive),
+ * match_x/match_y (that point's x, y; 0 for -1) and ambiguity
+ * (second / (best + 1e-6)) -- the reference's per-thread-row top-2 and row
+ * merge, bit-exact.  Descriptors: n x nfeatures f32 rows (nfeatures a
+ * multiple of 4, <= 128).  flags: SURFHIP_MATCH_FULL_TAIL also scores the
+ * last partial 32-point tile of set 2, which the reference drops
+ * (surfd.cu:2569); 0 follows the reference.  Scratch (surfhip_match_scratch
+ * bytes, device) is caller-provided (the call is then asynchronous), or
+ * NULL: the library allocates it and the call returns after the stream has
+ * finished the match. */
+#define SURFHIP_MATCH_FULL_TAIL 1
+size_t surfhip_match_scratch(int n1, int n2, int flags);
+int surfhip_match(surfhip_point* d_pts1, const surfhip_point* d_pts2, const float* d_feat1,
+                  const float* d_feat2, int n1, int n2, int nfeatures, int flags,
+                  void* d_scratch, void* stream);
+
 /* Library build identification (for the loaded-.so audit). */
 const char* surfhip_build_info(void);
 

@@ -81,6 +81,8 @@ _L.or_test_box.restype = C.c_uint32
 _L.or_test_box.argtypes = [_vp, _i, _i, _i, _i, _i]
 _L.or_test_place.argtypes = [_vp, _i, _i, C.c_float, _i, C.c_float, _i, C.c_float, C.c_float]
 
+_L.or_match.argtypes = [_vp, _vp, _vp, _vp, _i, _i, _i, _i]
+
 lib = _L
 
 
@@ -147,3 +149,19 @@ def bench_frames(p: Param, frames: np.ndarray, w: int, h: int, max_pts: int, nth
     secs = _L.or_bench_frames(C.byref(p), frames.ctypes.data, frames.shape[0], w, h, frames.shape[2],
                               frames.shape[1] * frames.shape[2], max_pts, nthreads, C.byref(tot))
     return secs, tot.value
+
+
+def match(pts1: np.ndarray, pts2: np.ndarray, f1: np.ndarray, f2: np.ndarray,
+          full_tail: bool = False) -> np.ndarray:
+    """or_match (findMaxCorr restated): a copy of pts1 with score, match,
+    match_x, match_y, ambiguity filled in."""
+    out = np.ascontiguousarray(pts1, dtype=POINT_DTYPE).copy()
+    pts2 = np.ascontiguousarray(pts2, dtype=POINT_DTYPE)
+    f1 = np.ascontiguousarray(f1, dtype=np.float32)
+    f2 = np.ascontiguousarray(f2, dtype=np.float32)
+    n1, n2 = len(out), len(pts2)
+    nf = f1.shape[1] if f1.ndim == 2 else (f2.shape[1] if f2.ndim == 2 else 64)
+    assert f1.shape == (n1, nf) and f2.shape == (n2, nf)
+    _L.or_match(out.ctypes.data, pts2.ctypes.data, f1.ctypes.data, f2.ctypes.data,
+                n1, n2, nf, int(bool(full_tail)))
+    return out

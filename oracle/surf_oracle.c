@@ -907,3 +907,61 @@ void or_test_place(float* desc, int wsz, int osz, float mag1, int ori1, float ma
 {
     place(desc, wsz, osz, mag1, ori1, mag2, ori2, rx, cx);
 }
+
+/* ------------------------------------------------------------- match --
+ * Surfor::match -> cuFindMaxCorr -> findMaxCorr (surf.cpp:418-428,
+ * surfd.cu:3554-3566, 2530-2656), restated per point of set 1.
+ *
+ * The reference block holds 32 points of set 1; its 8 thread rows (ty) each
+ * scan the set-2 points p2 with (p2 % 32) / 4 == ty of every FULL 32-point
+ * tile (`bp2 < num_pts2 - M7H + 1`, surfd.cu:2569: the last partial tile is
+ * dropped), in increasing p2, keeping (max, second, index) with strict `>`
+ * from (0, 0, -1) (surfd.cu:2607-2621).  Every score is one sequential fp32
+ * FMA chain over the descriptor (nvcc contracts `score += a * b`,
+ * surfd.cu:2596-2601, CMakeLists.txt passes no --fmad=false).  Row 0's
+ * state is then merged with rows 1..7 in order, ignoring the rows' second
+ * scores and rows whose index equals the running one (surfd.cu:2638-2655).
+ * Defined where the reference is not: points p1 >= n1 are not written
+ * (the reference writes a whole 32-point block), and index -1 (no positive
+ * score) gives match_x = match_y = 0 instead of reading surf2[-1].
+ * full_tail != 0 also scans the last partial tile (fixes the tile-tail bug;
+ * an option, the default follows the reference). */
+void or_match(or_point* pts1, const or_point* pts2, const float* f1, const float* f2,
+              int n1, int n2, int nf, int full_tail)
+{
+    const int ntile = full_tail ? (n2 + 31) / 32 : n2 / 32;
+    for (int p1 = 0; p1 < n1; p1++) {
+        const float* a = f1 + (size_t)p1 * nf;
+        float gmax[8], gsec[8];
+        int gidx[8];
+        for (int g = 0; g < 8; g++) {
+            float mx = 0.0f, sc = 0.0f;
+            int ix = -1;
+            for (int t = 0; t < ntile; t++) {
+                for (int dy = 0; dy < 4; dy++) {
+                    const int p2 = 32 * t + 4 * g + dy;
+                    if (p2 >= n2) continue;
+                    const float* b = f2 + (size_t)p2 * nf;
+                    float s = 0.0f;
+                    for (int d = 0; d < nf; d++) s = fmaf(a[d], b[d], s);
+                    if (s > mx) { sc = mx; mx = s; ix = p2; }
+                    else if (s > sc) sc = s;
+                }
+            }
+            gmax[g] = mx; gsec[g] = sc; gidx[g] = ix;
+        }
+        float mx = gmax[0], sc = gsec[0];
+        int ix = gidx[0];
+        for (int g = 1; g < 8; g++) {
+            if (ix == gidx[g]) continue;
+            if (gmax[g] > mx) { sc = fmaxf(mx, sc); mx = gmax[g]; ix = gidx[g]; }
+            else if (gmax[g] > sc) sc = gmax[g];
+        }
+        or_point* q = &pts1[p1];
+        q->score = mx;
+        q->match = ix;
+        q->match_x = ix >= 0 ? pts2[ix].x : 0.0f;
+        q->match_y = ix >= 0 ? pts2[ix].y : 0.0f;
+        q->ambiguity = sc / (mx + 1e-6f);
+    }
+}

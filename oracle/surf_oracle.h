@@ -148,6 +148,11 @@ int  or_detect_and_compute(const or_param* p, const uint8_t* img, int w, int h,
                            int pitch, or_point* pts, int max_pts, float* desc,
                            int* n_candidates);
 
+/* Surfor::match / findMaxCorr (surf.cpp:418-428, surfd.cu:2530-2656):
+ * writes score, match, match_x, match_y, ambiguity of pts1[0..n1). */
+void or_match(or_point* pts1, const or_point* pts2, const float* f1, const float* f2,
+              int n1, int n2, int nf, int full_tail);
+
 /* Deterministic sine/cosine used in place of __sinf/__cosf. */
 float or_sinf(float x);
 float or_cosf(float x);

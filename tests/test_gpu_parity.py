@@ -242,3 +242,110 @@ def test_surfor_mirror_api(surf, orc):
     assert desc_l2(got, o_desc).max() <= DESC_TOL
     surf.check(surf.lib.surfhip_free(dptr))
     surf.freeSurfData(data)
+
+
+# ------------------------------------------------------------------ match
+MATCH_FIELDS = ("score", "match", "match_x", "match_y", "ambiguity")
+
+
+def gpu_match(surf, p1, p2, f1, f2, flags=0, own_scratch=False):
+    n1, n2 = len(p1), len(p2)
+    nf = f1.shape[1]
+    b1 = surf.DeviceBuffer(max(48 * n1, 48))
+    b2 = surf.DeviceBuffer(max(48 * n2, 48))
+    d1 = surf.DeviceBuffer(max(f1.nbytes, 4))
+    d2 = surf.DeviceBuffer(max(f2.nbytes, 4))
+    if n1:
+        b1.upload(np.ascontiguousarray(p1))
+        d1.upload(np.ascontiguousarray(f1))
+    if n2:
+        b2.upload(np.ascontiguousarray(p2))
+        d2.upload(np.ascontiguousarray(f2))
+    scratch = None
+    if own_scratch:
+        scratch = surf.DeviceBuffer(max(surf.match_scratch_bytes(n1, n2, flags), 4))
+    surf.match_points(b1.ptr, b2.ptr, d1.ptr, d2.ptr, n1, n2, nf, flags, scratch.ptr if scratch else None)
+    surf.synchronize()
+    return b1.download(surf.POINT_DTYPE, n1) if n1 else np.zeros(0, surf.POINT_DTYPE)
+
+
+def assert_match_equal(got, ref):
+    for f in MATCH_FIELDS:
+        g, r = got[f], ref[f]
+        if g.dtype == np.float32:
+            g, r = g.view(np.uint32), r.view(np.uint32)
+        bad = np.nonzero(g != r)[0]
+        assert len(bad) == 0, f"{f} differs at {bad[:5]}"
+
+
+@pytest.mark.parametrize("tag,flags", [("ref", 0), ("full", 1)])
+def test_match_golden_left_right(surf, orc, tag, flags):
+    """Surfor::match of the reference's own image pair (main.cpp:250),
+    bit-exact against the committed oracle vectors."""
+    z = np.load(os.path.join(GOLDEN, "match_left_right_upright.npz"))
+    a = np.load(os.path.join(GOLDEN, "left_1280x960_upright.npz"))
+    b = np.load(os.path.join(GOLDEN, "right_1280x960_upright.npz"))
+    p1, p2 = a["points"].view(surf.POINT_DTYPE), b["points"].view(surf.POINT_DTYPE)
+    got = gpu_match(surf, p1, p2, a["desc"], b["desc"], flags)
+    ref = np.zeros(len(p1), surf.POINT_DTYPE)
+    for f in MATCH_FIELDS:
+        ref[f] = z[f"{tag}_{f}"]
+    assert_match_equal(got, ref)
+    # the detect fields are left untouched
+    for f in ("x", "y", "scale", "strength", "laplace"):
+        np.testing.assert_array_equal(got[f], p1[f])
+
+
+@pytest.mark.parametrize("n1,n2,nf,flags", [(1, 0, 64, 0), (7, 31, 64, 0), (7, 31, 64, 1), (300, 545, 64, 0),
+                                             (300, 545, 64, 1), (1000, 4096, 64, 0), (3000, 3000, 64, 1),
+                                             (257, 700, 128, 0), (129, 333, 36, 1), (64, 64, 16, 0)])
+def test_match_random_vs_oracle(surf, orc, n1, n2, nf, flags):
+    rng = np.random.default_rng(n1 + 7 * n2 + nf + flags)
+    f1 = rng.standard_normal((n1, nf)).astype(np.float32)
+    f2 = rng.standard_normal((n2, nf)).astype(np.float32)
+    f1 /= np.linalg.norm(f1, axis=1, keepdims=True)
+    if n2:
+        f2 /= np.linalg.norm(f2, axis=1, keepdims=True)
+        f2[n2 // 2] = f1[0]                          # a perfect partner (ties across rows)
+    p1 = np.zeros(n1, surf.POINT_DTYPE)
+    p1["x"] = rng.uniform(0, 100, n1)
+    p2 = np.zeros(n2, surf.POINT_DTYPE)
+    p2["x"] = rng.uniform(0, 1920, n2)
+    p2["y"] = rng.uniform(0, 1080, n2)
+    got = gpu_match(surf, p1, p2, f1, f2, flags, own_scratch=(n1 == 300))
+    ref = orc.match(p1, p2, f1, f2, full_tail=bool(flags))
+    assert_match_equal(got, ref)
+
+
+def test_surfor_match_end_to_end(surf, orc):
+    """Surfor.init -> detectAndCompute(left), detectAndCompute(right) ->
+    match (main.cpp:236-250) through the reference-shaped mirror."""
+    a = np.load(os.path.join(GOLDEN, "images.npz"))
+    d = surf.Surfor()
+    w, h = 1280, 960
+    d.init(4, 4.0, False, 9, 2, True, False, 4, w, h)
+    out = []
+    for key in ("left_1280x960", "right_1280x960"):
+        img = a[key]
+        data = surf.initSurfData(10000, True, True)
+        buf = surf.DeviceBuffer(img.nbytes)
+        buf.upload(img)
+        dptr = d.detectAndCompute(buf.ptr, data, (w, h, img.shape[1]), True)
+        out.append((data, dptr, buf))
+    (d1, f1, _), (d2, f2, _) = out
+    d.match(d1, d2, f1, f2)
+    z = np.load(os.path.join(GOLDEN, "match_left_right_upright.npz"))
+    # the GPU descriptors agree with the oracle's within 1e-4 L2, so scores
+    # may differ in the last bits; indices must agree where the best is clear
+    assert d1.num_pts == len(z["ref_match"])
+    got = d1.h_data[:d1.num_pts]
+    g1 = surf.download_ptr(f1, np.float32, d1.num_pts * 64).reshape(-1, 64)
+    g2 = surf.download_ptr(f2, np.float32, d2.num_pts * 64).reshape(-1, 64)
+    pts2 = surf.download_ptr(d2.d_data.ptr, surf.POINT_DTYPE, d2.num_pts)
+    ref = orc.match(got, pts2, g1, g2)                # oracle on the GPU's own descriptors: bit-exact
+    assert_match_equal(got, ref)
+    clear = z["ref_ambiguity"] < 0.99
+    assert (got["match"][clear] == z["ref_match"][clear]).mean() > 0.99
+    for data, dptr, _ in out:
+        surf.check(surf.lib.surfhip_free(dptr))
+        surf.freeSurfData(data)

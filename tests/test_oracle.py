@@ -249,3 +249,99 @@ def test_oracle_matches_golden(orc, name):
     assert_points_equal(pts, ref, fields=("x", "y", "scale", "o", "strength", "laplace", "ori"))
     assert desc_l2(desc, z["desc"]).max() == 0.0
     assert nc == int(z["meta"][2])
+
+
+# ------------------------------------------------------------------ match
+def _np_match(f1, f2, full_tail=False):
+    """Independent restatement of findMaxCorr (surfd.cu:2530-2656) for inputs
+    whose dot products are exact in fp32 (dyadic values): every score is the
+    exact integer-scaled sum, so the FMA chain order cannot matter.  Thread
+    row g of the reference block sees the p2 with (p2 % 32) // 4 == g of the
+    full tiles (surfd.cu:2569), top-2 by strict '>' from (0, 0, -1), rows
+    merged in order ignoring their second scores (surfd.cu:2638-2655)."""
+    n1, n2 = len(f1), len(f2)
+    nscan = n2 if full_tail else 32 * (n2 // 32)
+    scores = (f1.astype(np.float64) @ f2.astype(np.float64).T)[:, :nscan]
+    rows = (np.arange(nscan) % 32) // 4
+    out = []
+    for p1 in range(n1):
+        states = []
+        for g in range(8):
+            idx = np.nonzero(rows == g)[0]
+            mx, sc, ix = 0.0, 0.0, -1
+            for p2 in idx:
+                s = scores[p1, p2]
+                if s > mx:
+                    sc, mx, ix = mx, s, int(p2)
+                elif s > sc:
+                    sc = s
+            states.append((mx, sc, ix))
+        M, S, I = states[0]
+        for mx, _sc, ix in states[1:]:
+            if ix == I:
+                continue
+            if mx > M:
+                S, M, I = max(M, S), mx, ix
+            elif mx > S:
+                S = mx
+        out.append((M, S, I))
+    return out
+
+
+@pytest.mark.parametrize("n1,n2,nf,full", [(37, 100, 64, False), (37, 100, 64, True), (5, 31, 64, False),
+                                            (5, 31, 64, True), (64, 96, 128, False), (20, 70, 36, True)])
+def test_match_vs_numpy_exact(orc, n1, n2, nf, full):
+    rng = np.random.default_rng(n1 * 1000 + n2 + nf + full)
+    # multiples of 1/8 in [-1, 1]: products are multiples of 1/64, sums stay
+    # far below 2^24 / 64, so every fp32 FMA chain is exact
+    f1 = (rng.integers(-8, 9, (n1, nf)) / 8).astype(np.float32)
+    f2 = (rng.integers(-8, 9, (n2, nf)) / 8).astype(np.float32)
+    f2[7] = f1[3]                                      # exact duplicate -> ties within rows
+    f2[min(40, n2 - 1)] = f1[3]
+    p1 = np.zeros(n1, orc.POINT_DTYPE)
+    p2 = np.zeros(n2, orc.POINT_DTYPE)
+    p2["x"] = np.arange(n2) + 0.5
+    p2["y"] = -np.arange(n2) - 0.25
+    got = orc.match(p1, p2, f1, f2, full_tail=full)
+    ref = _np_match(f1, f2, full)
+    for i, (M, S, I) in enumerate(ref):
+        assert got["match"][i] == I, i
+        assert got["score"][i] == np.float32(M), i
+        assert got["ambiguity"][i] == np.float32(np.float32(S) / (np.float32(M) + np.float32(1e-6))), i
+        assert got["match_x"][i] == (p2["x"][I] if I >= 0 else 0.0)
+        assert got["match_y"][i] == (p2["y"][I] if I >= 0 else 0.0)
+    if n2 < 32 and not full:                           # no full tile: nothing is scored
+        assert (got["match"] == -1).all()
+
+
+def test_match_tail_bug_is_the_default(orc):
+    """The reference never scores the last partial tile of set 2
+    (surfd.cu:2569): a perfect partner there is not found by default."""
+    rng = np.random.default_rng(3)
+    f = rng.standard_normal((40, 64)).astype(np.float32)
+    f /= np.linalg.norm(f, axis=1, keepdims=True)
+    p = np.zeros(40, orc.POINT_DTYPE)
+    q = orc.match(p[35:36], p, f[35:36], f)
+    assert q["match"][0] != 35
+    q = orc.match(p[35:36], p, f[35:36], f, full_tail=True)
+    assert q["match"][0] == 35
+
+
+def test_match_golden_fixture(orc):
+    z = np.load(os.path.join(GOLDEN, "match_left_right_upright.npz"))
+    a = np.load(os.path.join(GOLDEN, "left_1280x960_upright.npz"))
+    b = np.load(os.path.join(GOLDEN, "right_1280x960_upright.npz"))
+    p1, p2 = a["points"].view(orc.POINT_DTYPE), b["points"].view(orc.POINT_DTYPE)
+    for tag, full in (("ref", False), ("full", True)):
+        m = orc.match(p1, p2, a["desc"], b["desc"], full_tail=full)
+        for f in ("score", "match", "match_x", "match_y", "ambiguity"):
+            np.testing.assert_array_equal(m[f].view(np.uint32) if m[f].dtype == np.float32 else m[f],
+                                          z[f"{tag}_{f}"].view(np.uint32) if z[f"{tag}_{f}"].dtype == np.float32
+                                          else z[f"{tag}_{f}"])
+    # left/right overlap with a ~(532, -18) px shift: the unambiguous matches
+    # (ambiguity < 0.9) agree on that displacement
+    s = z["ref_ambiguity"] < 0.9
+    dx = p1["x"][s] - z["ref_match_x"][s]
+    dy = p1["y"][s] - z["ref_match_y"][s]
+    assert s.sum() > 100
+    assert ((abs(dx - np.median(dx)) < 40) & (abs(dy - np.median(dy)) < 40)).mean() > 0.95
