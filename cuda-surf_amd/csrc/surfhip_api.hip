@@ -51,7 +51,11 @@ struct surfhip_detector {
     OctaveParams* d_oct = nullptr;      // device copy read by the fused launches
     LaunchPlan plan{};
     FarPlan far{};
-    int W = 0, H = 0, max_batch = 0, max_pts = 0, cap = 0;
+    int W = 0, H = 0, max_batch = 0, max_pts = 0, cap = 0;   // W x H: the frames the integral is taken of
+    int srcW = 0, srcH = 0;             // the caller's frames (= W x H unless doubled)
+    uint8_t* dbl = nullptr;             // doubled: the (2 srcW - 2) x (2 srcH - 2) frames D
+    int dpitch = 0;
+    long long dstride = 0;
     int nbands = 0, CW = 0;
     size_t tot_osize = 0;
     int32_t* ii = nullptr;
@@ -249,15 +253,14 @@ int surfhip_make_param(surfhip_param* out, int noctaves, float thresh, int doubl
 {
     if (!out) return SURFHIP_ERR_INVALID;
     memset(out, 0, sizeof(*out));
-    if (doubled) return SURFHIP_ERR_UNSUPPORTED;   // doubled-image integral: SURVEY.md 8f rank 2
     if (noctaves < 1 || noctaves > kMaxOct || desc_wsz < 1 || 12 % desc_wsz != 0 || sampling_step < 1)
         return SURFHIP_ERR_INVALID;
-    out->doubled = false;
+    out->doubled = doubled != 0;
     out->noctaves = noctaves;
-    out->divisor = 1.f;
+    out->divisor = doubled ? 0.5f : 1.f;
     out->init_lobe = init_mask_size / 3;
     out->max_scale = out->init_lobe + 2;
-    out->sampling = sampling_step;
+    out->sampling = sampling_step + (doubled ? sampling_step : 0);
     out->thresh = thresh;
     out->upright = upright != 0;
     out->extend = extend != 0;
@@ -381,7 +384,7 @@ static void free_all(surfhip_detector* d)
 {
     void* ptrs[] = {d->d_oct, d->ii, d->resp, d->colsum, d->cand, d->keys, d->gscratch, d->cand_count,
                     d->scan_key, d->scan_src, d->item_count, d->item_off,
-                    d->offsets, d->order, d->status, d->pts1, d->desc1, d->count1};
+                    d->offsets, d->order, d->status, d->pts1, d->desc1, d->count1, d->dbl};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (int i = 0; i < SURFHIP_NSTAGE; i++)
@@ -398,12 +401,21 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     if (width + 1 > 4096) return SURFHIP_ERR_UNSUPPORTED;     // integral kernel: <= 16 columns per thread
     surfhip_param chk;
     int rc = surfhip_make_param(&chk, param->noctaves, param->thresh, param->doubled, param->init_lobe * 3,
-                                param->sampling, param->upright, param->extend, param->desc_wsz);
+                                param->doubled ? param->sampling / 2 : param->sampling, param->upright,
+                                param->extend, param->desc_wsz);
     if (rc != SURFHIP_OK) return rc;
     surfhip_detector* d = new surfhip_detector();
     d->param = chk;
-    d->W = width;
-    d->H = height;
+    d->srcW = width;
+    d->srcH = height;
+    // doubled (surf.cpp:234-235, 377-378): the integral is taken of the
+    // (2W-2) x (2H-2) upsampled frames D, giving the (2W-1) x (2H-1) grid
+    d->W = chk.doubled ? 2 * width - 2 : width;
+    d->H = chk.doubled ? 2 * height - 2 : height;
+    if (d->W + 1 > 4096) {
+        delete d;
+        return SURFHIP_ERR_UNSUPPORTED;
+    }
     d->max_batch = max_batch;
     d->max_pts = max_pts;
     int cap = cand_cap > 0 ? cand_cap : std::max(max_pts, kSortCap);
@@ -418,8 +430,8 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
         delete d;
         return rc;
     }
-    d->nbands = (height + kBandRows - 1) / kBandRows;
-    d->CW = (width + 1 <= 2048) ? 2048 : 4096;
+    d->nbands = (d->H + kBandRows - 1) / kBandRows;
+    d->CW = (d->W + 1 <= 2048) ? 2048 : 4096;
     const size_t B = (size_t)max_batch;
 #define ALLOC(ptr, bytes)                                    \
     do {                                                     \
@@ -447,6 +459,11 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     ALLOC(d->desc1, (size_t)max_pts * d->param.nfeatures * sizeof(float));
     ALLOC(d->count1, 16);
     if (d->cap > kSortCap) ALLOC(d->gscratch, B * d->cap * sizeof(uint64_t));
+    if (d->param.doubled) {
+        d->dpitch = align_up(d->W, 128);
+        d->dstride = (long long)d->H * d->dpitch;
+        ALLOC(d->dbl, B * (size_t)d->dstride);
+    }
 #undef ALLOC
     // zero once: integral pad columns and response pad columns are never
     // written by the kernels and never read by them either
@@ -502,16 +519,30 @@ int surfhip_detector_set_stream(surfhip_detector* d, void* stream)
 static int check_frames(surfhip_detector* d, const uint8_t* frames, int nframes, int pitch, size_t stride)
 {
     if (!d || !frames || nframes < 1 || nframes > d->max_batch) return SURFHIP_ERR_INVALID;
-    if (pitch < d->W || (pitch & 15) != 0) return SURFHIP_ERR_INVALID;
+    if (pitch < d->srcW || (pitch & 15) != 0) return SURFHIP_ERR_INVALID;
     if (((uintptr_t)frames & 15) != 0) return SURFHIP_ERR_INVALID;
-    if (nframes > 1 && (stride < (size_t)pitch * d->H || (stride & 15) != 0)) return SURFHIP_ERR_INVALID;
+    if (nframes > 1 && (stride < (size_t)pitch * d->srcH || (stride & 15) != 0)) return SURFHIP_ERR_INVALID;
     return SURFHIP_OK;
+}
+
+// doubled: upsample the caller's frames into d->dbl and continue from there
+static hipError_t source_frames(surfhip_detector* d, const uint8_t*& frames, int& pitch, size_t& stride,
+                                int nframes, hipStream_t s)
+{
+    if (!d->param.doubled) return hipSuccess;
+    hipError_t e = launch_double(frames, pitch, (long long)stride, nframes, d->srcW, d->srcH, d->dbl, d->dpitch,
+                                 d->dstride, s);
+    frames = d->dbl;
+    pitch = d->dpitch;
+    stride = (size_t)d->dstride;
+    return e;
 }
 
 int surfhip_run_integral(surfhip_detector* d, const uint8_t* frames, int nframes, int pitch, size_t stride)
 {
     int rc = check_frames(d, frames, nframes, pitch, stride);
     if (rc) return rc;
+    HIPCHK(source_frames(d, frames, pitch, stride, nframes, d->stream));
     HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, d->stream));
     d->last_frames = frames;
     d->last_pitch = pitch;
@@ -540,6 +571,7 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
     if (prof) {
         // serial, so that the stage events bracket each stage alone
         HIPCHK(hipEventRecord(d->ev[0], s));
+        HIPCHK(source_frames(d, frames, pitch, stride, nframes, s));
         HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, s));
         HIPCHK(hipEventRecord(d->ev[1], s));
         HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
@@ -549,6 +581,7 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
         // the u8 Hessian kernels (octaves 0, 1) need no integral image: they run
         // on s beside the integral and the integral-image Hessian kernels
         // (octaves >= 2) on the side stream; s waits for both
+        HIPCHK(source_frames(d, frames, pitch, stride, nframes, s));
         HIPCHK(hipEventRecord(d->fork, s));
         HIPCHK(hipStreamWaitEvent(d->side, d->fork, 0));
         HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, d->side));

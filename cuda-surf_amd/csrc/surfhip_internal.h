@@ -109,6 +109,10 @@ hipError_t launch_sort(const surfhip_point* cand, const uint32_t* keys, uint64_t
 hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
                            const int* counts, const int* offsets, const int* order, int nframes, float* desc,
                            hipStream_t s);
+// Doubled-image input (surfhip_double.hip): frames (W x H) -> D ((2W-2) x
+// (2H-2) u8, row pitch dpitch, a multiple of 4).
+hipError_t launch_double(const uint8_t* frames, int pitch, long long fstride, int nframes, int W, int H,
+                         uint8_t* dst, int dpitch, long long dstride, hipStream_t s);
 // Descriptor matching (surfhip_match.hip): scratch = match_scratch_bytes().
 size_t match_scratch_bytes(int n1, int n2, int flags);
 hipError_t launch_match(surfhip_point* pts1, const surfhip_point* pts2, const float* f1, const float* f2, int n1,

@@ -115,7 +115,8 @@ int surfhip_detector_destroy(surfhip_detector* det);
 int surfhip_detector_set_stream(surfhip_detector* det, void* stream);
 
 /* Surfor::init parameter derivation (surf.cpp:63-79); returns
- * SURFHIP_ERR_UNSUPPORTED for doubled=true (out of scope). */
+ * SURFHIP_ERR_UNSUPPORTED for max_scale != 5 or more than 128 features;
+ * doubled = true doubles the sampling step and halves the divisor. */
 int surfhip_make_param(surfhip_param* out, int noctaves, float thresh, int doubled,
                        int init_mask_size, int sampling_step, int upright,
                        int extend, int desc_wsz);

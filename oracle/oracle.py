@@ -81,6 +81,7 @@ _L.or_test_box.restype = C.c_uint32
 _L.or_test_box.argtypes = [_vp, _i, _i, _i, _i, _i]
 _L.or_test_place.argtypes = [_vp, _i, _i, C.c_float, _i, C.c_float, _i, C.c_float, C.c_float]
 
+_L.or_double_image.argtypes = [_vp, _i, _i, _i, _vp, _i]
 _L.or_match.argtypes = [_vp, _vp, _vp, _vp, _i, _i, _i, _i]
 
 lib = _L
@@ -121,10 +122,21 @@ def integral(img: np.ndarray, w: int, h: int) -> np.ndarray:
     return ii
 
 
+def double_image(img: np.ndarray, w: int, h: int) -> np.ndarray:
+    """The doubled image D (2h-2 rows x 2w-2 columns, u8) of cuIntegralDoubleU4."""
+    img = np.ascontiguousarray(img)
+    out = np.zeros((2 * h - 2, 2 * w - 2), np.uint8)
+    _L.or_double_image(img.ctypes.data, w, h, img.shape[1], out.ctypes.data, out.shape[1])
+    return out
+
+
 def hessian(p: Param, img: np.ndarray, w: int, h: int):
     """Integral image + all response planes (flat float array, reference layout)."""
     g, octs = geometry(p, w, h)
-    ii = integral(img, w, h)
+    if p.doubled:                                    # surf.cpp:234-235
+        ii = integral(double_image(img, w, h), 2 * w - 2, 2 * h - 2)
+    else:
+        ii = integral(img, w, h)
     resp = np.zeros(g.tot_osize, np.float32)
     _L.or_hessian(C.byref(p), C.byref(g), octs, ii.ctypes.data, resp.ctypes.data)
     return ii, resp, g, octs

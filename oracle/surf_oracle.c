@@ -49,7 +49,6 @@ int or_init_param(or_param* p, int noctaves, float thresh, bool doubled,
                   bool extend, int desc_wsz)
 {
     memset(p, 0, sizeof(*p));
-    if (doubled) return -1;                       /* out of scope */
     if (noctaves < 1 || noctaves > OR_MAX_OCTAVE) return -1;
     if (desc_wsz < 1 || 12 % desc_wsz != 0) return -1;
     p->doubled = doubled;
@@ -83,8 +82,8 @@ void or_init_tables(float lut1[83], float lut2[40], float bins[OR_NBIN])
 void or_geometry(const or_param* p, int w, int h, or_geom* g)
 {
     memset(g, 0, sizeof(*g));
-    g->iwhp.x = w + 1;
-    g->iwhp.y = h + 1;
+    g->iwhp.x = p->doubled ? w + w - 1 : w + 1;       /* surf.cpp:377-378 */
+    g->iwhp.y = p->doubled ? h + h - 1 : h + 1;
     g->iwhp.z = align_up(g->iwhp.x, 128);
     g->swhp[0].x = (g->iwhp.x - 1) / p->sampling;
     g->swhp[0].y = (g->iwhp.y - 1) / p->sampling;
@@ -177,6 +176,41 @@ void or_integral(const uint8_t* img, int w, int h, int pitch, int32_t* ii, int i
         for (int x = 0; x < w; x++) {
             row += src[x];
             dst[x + 1] = up[x + 1] + row;   /* column pass folded in */
+        }
+    }
+}
+
+/* Doubled image (cuIntegralDoubleU4, surfd.cu:2707-2772): the first kernel
+ * (integralDoubleRow0U2, surfd.cu:166-209) writes, for source pixel (y, x),
+ * integral rows 2y+1 / 2y+2 and columns 2x+1 / 2x+2 from the 2x upsampled
+ * image D with
+ *   D[2y][2x]     = s[y][x]
+ *   D[2y][2x+1]   = rn((s[y][x] + s[y][x+1]) * 0.5f)
+ *   D[2y+1][2x]   = rn((s[y][x] + s[y+1][x]) * 0.5f)
+ *   D[2y+1][2x+1] = rn((s[y][x] + s[y][x+1] + s[y+1][x] + s[y+1][x+1]) * 0.25f)
+ * (__float2int_rn: round half to even) as running sums inside groups of 4
+ * columns; integralRow1U4/Row2U4 (surfd.cu:212-259) chain the groups into
+ * a row prefix and integralCol0U4/Col1U4/Col2U4 (surfd.cu:262-318) do the
+ * same down the columns.  Net: ii = the integral of D over the
+ * (2w-1) x (2h-1) integral grid (surf.cpp:377-378), i.e. D is
+ * (2w-2) x (2h-2) and never needs s outside the image (the reference's
+ * writes to integral row 2h-1 / 2h and column 2w-1 / 2w, which read source
+ * row h / column w, fall outside that grid and are dropped here). */
+void or_double_image(const uint8_t* img, int w, int h, int pitch, uint8_t* dst, int dpitch)
+{
+    const int W2 = 2 * w - 2, H2 = 2 * h - 2;
+    for (int r = 0; r < H2; r++) {
+        const int y = r >> 1;
+        const uint8_t* s0 = img + (size_t)y * pitch;
+        const uint8_t* s1 = (r & 1) ? s0 + pitch : s0;
+        for (int c = 0; c < W2; c++) {
+            const int x = c >> 1;
+            int v;
+            if (!(r & 1) && !(c & 1)) v = s0[x];
+            else if (!(r & 1)) v = (int)rintf((float)(s0[x] + s0[x + 1]) * 0.5f);
+            else if (!(c & 1)) v = (int)rintf((float)(s0[x] + s1[x]) * 0.5f);
+            else v = (int)rintf((float)(s0[x] + s0[x + 1] + s1[x] + s1[x + 1]) * 0.25f);
+            dst[(size_t)r * dpitch + c] = (uint8_t)v;
         }
     }
 }
@@ -823,7 +857,17 @@ int or_detect_and_compute(const or_param* p, const uint8_t* img, int w, int h,
     int32_t* ii = (int32_t*)calloc((size_t)g.iwhp.y * g.iwhp.z, sizeof(int32_t));
     float* resp = (float*)calloc(g.tot_osize, sizeof(float));
     if (!ii || !resp) { free(ii); free(resp); return -1; }
-    or_integral(img, w, h, pitch, ii, g.iwhp.z);
+    if (p->doubled) {                                 /* surf.cpp:234-235 */
+        if (w < 2 || h < 2) { free(ii); free(resp); return -1; }
+        const int dp = g.iwhp.z;
+        uint8_t* dimg = (uint8_t*)malloc((size_t)(2 * h - 2) * dp);
+        if (!dimg) { free(ii); free(resp); return -1; }
+        or_double_image(img, w, h, pitch, dimg, dp);
+        or_integral(dimg, 2 * w - 2, 2 * h - 2, dp, ii, g.iwhp.z);
+        free(dimg);
+    } else {
+        or_integral(img, w, h, pitch, ii, g.iwhp.z);
+    }
     or_hessian(p, &g, oct, ii, resp);
     int cand = or_find_points(p, &g, oct, ii, resp, pts, max_pts);
     int n = cand < max_pts ? cand : max_pts;

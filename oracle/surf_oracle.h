@@ -119,6 +119,10 @@ void or_octave_params(const or_param* p, const or_geom* g, or_octave oct[OR_MAX_
 /* integralRow + integralCol (surfd.cu:129-165): ii is (H+1) x ipitch int32. */
 void or_integral(const uint8_t* img, int w, int h, int pitch,
                  int32_t* ii, int ipitch);
+/* The doubled image D of cuIntegralDoubleU4 (surfd.cu:166-318, 2707-2772):
+ * (2w-2) x (2h-2) u8, row pitch dpitch; integral(D) is the reference's
+ * doubled integral image. */
+void or_double_image(const uint8_t* img, int w, int h, int pitch, uint8_t* dst, int dpitch);
 /* All response planes of all octaves (halfImage + calcHessianMultiConst,
  * surf.cpp:248-294, surfd.cu:321-331, 445-481).  resp has g->tot_osize floats
  * and is fully overwritten (zeros outside each scale's valid window). */

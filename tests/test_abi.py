@@ -58,18 +58,17 @@ def test_make_param_matches_oracle(surf, orc):
         for upright in (False, True):
             for extend in (False, True):
                 for wsz in (2, 3, 4, 6):
-                    b = orc.make_param(noct, 4.0, False, 9, 2, upright, extend, wsz)
-                    if b.nfeatures > 128:          # the wave-per-keypoint descriptor holds <= 128
-                        with pytest.raises(surf.SurfError):
-                            surf.make_param(noct, 4.0, False, 9, 2, upright, extend, wsz)
-                        continue
-                    a = surf.make_param(noct, 4.0, False, 9, 2, upright, extend, wsz)
-                    assert bytes(a) == bytes(b)
+                    for dbl in (False, True):
+                        b = orc.make_param(noct, 4.0, dbl, 9, 2, upright, extend, wsz)
+                        if b.nfeatures > 128:          # the wave-per-keypoint descriptor holds <= 128
+                            with pytest.raises(surf.SurfError):
+                                surf.make_param(noct, 4.0, dbl, 9, 2, upright, extend, wsz)
+                            continue
+                        a = surf.make_param(noct, 4.0, dbl, 9, 2, upright, extend, wsz)
+                        assert bytes(a) == bytes(b)
 
 
 def test_make_param_rejects_out_of_scope(surf):
-    with pytest.raises(surf.SurfError):
-        surf.make_param(4, 4.0, doubled=True)
     with pytest.raises(surf.SurfError):
         surf.make_param(4, 4.0, init_mask_size=12)     # max_scale != 5
     with pytest.raises(surf.SurfError):

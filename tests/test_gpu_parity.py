@@ -349,3 +349,50 @@ def test_surfor_match_end_to_end(surf, orc):
     for data, dptr, _ in out:
         surf.check(surf.lib.surfhip_free(dptr))
         surf.freeSurfData(data)
+
+
+# ---------------------------------------------------------- doubled image
+@pytest.mark.parametrize("w,h", [(64, 48), (333, 211), (1920, 1080)])
+def test_doubled_integral_and_planes_bit_exact(surf, orc, w, h):
+    """doubled = true (surf.cpp:234-235, cuIntegralDoubleU4 surfd.cu:2707-2772):
+    the (2W-1) x (2H-1) integral image and every response plane."""
+    frames = surf.synth_frames(2, w, h, first=31)
+    param = surf.make_param(4, 4.0, doubled=True, upright=True)
+    res = gpu_run(surf, param, frames, w, h, want_ws=True, desc=False)
+    op = orc.make_param(4, 4.0, doubled=True, upright=True)
+    for f in range(2):
+        ii, ref, g, octs = orc.hessian(op, frames[f], w, h)
+        assert (g.iwhp.x, g.iwhp.y) == (2 * w - 1, 2 * h - 1)
+        got_ii = res["ii"][f][:ii.size].reshape(ii.shape)
+        np.testing.assert_array_equal(got_ii, ii)
+        got = res["resp"][f]
+        for (o, s, rp), (_, _, gp) in zip(_plane_views(ref, g, octs, op), _plane_views(got, g, octs, op)):
+            same = rp.view(np.uint32) == gp.view(np.uint32)
+            assert same.all(), f"octave {o} scale {s}: {(~same).sum()} cells differ"
+
+
+@pytest.mark.parametrize("upright,extend", [(True, False), (False, False), (True, True)])
+def test_doubled_detect_describe(surf, orc, upright, extend):
+    w, h = 640, 480
+    frames = surf.synth_frames(2, w, h, first=140)
+    param = surf.make_param(4, 4.0, doubled=True, upright=upright, extend=extend)
+    res = gpu_run(surf, param, frames, w, h)
+    op = orc.make_param(4, 4.0, doubled=True, upright=upright, extend=extend)
+    for f in range(2):
+        o_pts, o_desc, nc = orc.detect(op, frames[f], w, h)
+        assert res["cand"][f] == nc and nc > 100
+        compare_frame(res["pts"][f], res["desc"][f], o_pts, o_desc, upright)
+
+
+def test_doubled_reference_image(surf, orc):
+    """The reference's 640x480 left image with doubled = true."""
+    img = np.load(os.path.join(GOLDEN, "images.npz"))["left_640x480"]
+    w, h = 640, 480
+    frames = np.zeros((1, h, 640), np.uint8)
+    frames[0] = img
+    param = surf.make_param(4, 4.0, doubled=True, upright=True)
+    res = gpu_run(surf, param, frames, w, h)
+    op = orc.make_param(4, 4.0, doubled=True, upright=True)
+    o_pts, o_desc, nc = orc.detect(op, img, w, h)
+    assert res["cand"][0] == nc
+    compare_frame(res["pts"][0], res["desc"][0], o_pts, o_desc, True)

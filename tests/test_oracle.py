@@ -30,8 +30,8 @@ def test_init_params_match_reference_defaults(orc):
     assert p.divisor == 1.0
     p = orc.make_param(5, 4.0, False, 9, 2, False, True, 4)
     assert (p.orient_size, p.nfeatures) == (8, 128)
-    with pytest.raises(ValueError):
-        orc.make_param(4, 4.0, True)           # doubled: out of scope
+    p = orc.make_param(4, 4.0, True, 9, 2)     # doubled (surf.cpp:69, 72)
+    assert (p.sampling, p.divisor, p.doubled) == (4, 0.5, True)
 
 
 def test_geometry_1080p_matches_survey(orc):
@@ -345,3 +345,115 @@ def test_match_golden_fixture(orc):
     dy = p1["y"][s] - z["ref_match_y"][s]
     assert s.sum() > 100
     assert ((abs(dx - np.median(dx)) < 40) & (abs(dy - np.median(dy)) < 40)).mean() > 0.95
+
+
+# ---------------------------------------------------------- doubled image
+def _sim_reference_double_integral(img):
+    """Literal simulation of cuIntegralDoubleU4's six kernels
+    (surfd.cu:166-318, launch geometry surfd.cu:2707-2772) on a zeroed
+    buffer with spare rows, every thread of every launch run in turn (no
+    thread reads what another thread of the same launch writes)."""
+    h1, w1 = img.shape
+    src = np.zeros((h1 + 1, w1 + 2), np.int64)          # the reads past the image see 0
+    src[:h1, :w1] = img
+    w2, h2 = 2 * w1 - 1, 2 * h1 - 1
+    p2 = (w2 + 127) // 128 * 128
+    dst = np.zeros(((h2 + 3) * p2,), np.int64)         # spare rows take the OOB writes
+
+    def rn(v):
+        return int(np.rint(np.float32(v)))
+    # integralDoubleRow0U2: thread (ix, iy), bix = 2 ix
+    for iy in range(h1):
+        for bix in range(0, w1, 2):
+            S = lambda y, x: int(src[y, x])
+            w_ = (2 * iy + 1) * p2 + 2 * bix + 1
+            x_, y_, z_ = w_ + 1, w_ + p2, w_ + p2 + 1
+            s00, s01, s10, s11 = S(iy, bix), S(iy, bix + 1), S(iy + 1, bix), S(iy + 1, bix + 1)
+            dst[w_] = s00
+            dst[y_] = rn(np.float32(s00 + s10) * np.float32(0.5))
+            if bix + 1 >= w1:
+                continue
+            dst[x_] = dst[w_] + rn(np.float32(s00 + s01) * np.float32(0.5))
+            dst[z_] = dst[y_] + rn(np.float32(s00 + s01 + s10 + s11) * np.float32(0.25))
+            s00, s01, s10, s11 = s01, S(iy, bix + 2), s11, S(iy + 1, bix + 2)
+            w_, x_, y_, z_ = w_ + 2, x_ + 2, y_ + 2, z_ + 2
+            dst[w_] = dst[w_ - 1] + s00
+            dst[y_] = dst[y_ - 1] + rn(np.float32(s00 + s10) * np.float32(0.5))
+            if bix + 2 >= w1:
+                continue
+            dst[x_] = dst[w_] + rn(np.float32(s00 + s01) * np.float32(0.5))
+            dst[z_] = dst[y_] + rn(np.float32(s00 + s01 + s10 + s11) * np.float32(0.25))
+    # integralRow1U4: per row iy >= 1, chain the ends of the 4-column groups
+    for iy in range(1, h2):
+        i = iy * p2 + 1 + 3
+        j, k = i + 4, 8
+        while k < w2:
+            dst[j] += dst[i]
+            i, j, k = j, j + 4, k + 4
+    # integralRow2U4: add the previous group's end to columns 4(ix+1)+1 .. +3
+    for iy in range(1, h2):
+        for ix in range(0, (w2 - 1) // 4 + 1):
+            bix = (ix + 1) * 4 + 1
+            if bix >= w2:
+                continue
+            idx = iy * p2 + bix - 1
+            for t in range(3):
+                if bix + t >= w2:
+                    break
+                dst[idx + 1 + t] += dst[idx]
+    # integralCol0U4: within groups of 4 rows starting at row 1
+    for ix in range(1, w2):
+        for iy in range(0, (h2 - 1) // 4 + 1):
+            biy = iy * 4 + 1
+            if biy + 1 >= h2:
+                continue
+            idx = biy * p2 + ix
+            for t in range(3):
+                if biy + 1 + t >= h2:
+                    break
+                dst[idx + p2] += dst[idx]
+                idx += p2
+    # integralCol1U4: chain the group ends (rows 4, 8, ...)
+    for ix in range(1, w2):
+        i = ix + 4 * p2
+        j, k = i + 4 * p2, 8
+        while k < h2:
+            dst[j] += dst[i]
+            i, j, k = j, j + 4 * p2, k + 4
+    # integralCol2U4: add the previous group's end to rows 4(iy+1)+1 .. +3
+    for ix in range(1, w2):
+        for iy in range(0, (h2 - 1) // 4 + 1):
+            biy = (iy + 1) * 4 + 1
+            if biy >= h2:
+                continue
+            idx = (biy - 1) * p2 + ix
+            for t in range(3):
+                if biy + t >= h2:
+                    break
+                dst[idx + (1 + t) * p2] += dst[idx]
+    return dst[:h2 * p2].reshape(h2, p2)[:, :w2].astype(np.uint32).view(np.int32)
+
+
+@pytest.mark.parametrize("h,w", [(7, 9), (6, 10), (9, 12), (5, 5)])
+def test_doubled_integral_vs_reference_kernels(orc, h, w):
+    """or_double_image + or_integral equals a literal run of the reference's
+    six doubled-integral kernels on the (2w-1) x (2h-1) grid."""
+    rng = np.random.default_rng(h * 100 + w)
+    img = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    img[0, 0], img[-1, -1] = 255, 1                   # odd sums: exercise round-half-even
+    ref = _sim_reference_double_integral(img)
+    D = orc.double_image(img, w, h)
+    got = orc.integral(D, 2 * w - 2, 2 * h - 2)[:, :2 * w - 1]
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_doubled_detect_geometry(orc):
+    p = orc.make_param(4, 4.0, doubled=True, upright=True)
+    assert p.sampling == 4 and p.divisor == np.float32(0.5)
+    g, _ = orc.geometry(p, 640, 480)
+    assert (g.iwhp.x, g.iwhp.y, g.iwhp.z) == (1279, 959, 1280)      # surf.cpp:377-379
+    assert (g.swhp[0].x, g.swhp[0].y) == (319, 239)
+    img = np.load(os.path.join(GOLDEN, "images.npz"))["left_640x480"]
+    pts, d, nc = orc.detect(p, img, 640, 480)
+    assert len(pts) > 500 and nc == len(pts)
+    assert pts["x"].max() < 640 and pts["y"].max() < 480       # coordinates in source pixels
