@@ -116,6 +116,13 @@ _sigs = {
     "surfhip_pack_slab": (_i, [_vp, _vp, _vp, _vp, _i, _vp]),
     "surfhip_match_scratch": (_sz, [_i, _i, _i]),
     "surfhip_match": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp]),
+    "surfhip_ingest_create": (_i, [C.POINTER(_vp), _vp, _i]),
+    "surfhip_ingest_destroy": (_i, [_vp]),
+    "surfhip_ingest_acquire": (_i, [_vp, C.POINTER(_vp), C.POINTER(_i), C.POINTER(_sz)]),
+    "surfhip_ingest_submit": (_i, [_vp, _i]),
+    "surfhip_ingest_collect": (_i, [_vp, C.POINTER(_vp), C.POINTER(_sz)]),
+    "surfhip_ingest_pending": (_i, [_vp, C.POINTER(_i)]),
+    "surfhip_dump_append": (_i, [C.c_char_p, _vp, _sz, _i, _i, C.POINTER(SurfParam), C.c_longlong]),
     "surfhip_build_info": (C.c_char_p, []),
 }
 for _name, (_res, _args) in _sigs.items():
@@ -481,6 +488,93 @@ def build_slab(counts: np.ndarray, pts: np.ndarray, desc) -> np.ndarray:
     out[head:head + 48 * total] = np.ascontiguousarray(pts[:total]).view(np.uint8)
     if nf:
         out[head + 48 * total:] = np.ascontiguousarray(desc[:total], dtype=np.float32).view(np.uint8).ravel()
+    return out
+
+
+class Ingest:
+    """Pipelined host-frame ring over one Detector (surfhip_ingest_*):
+    `acquire()` gives a pinned u8 view [max_batch, H, pitch] to fill,
+    `submit(n)` queues H2D + detect + pack, `collect()` returns the oldest
+    batch's result slab (a host copy; parse with parse_slab)."""
+
+    def __init__(self, det: "Detector", depth: int = 2):
+        self.det, self.depth = det, depth
+        h = C.c_void_p()
+        check(_lib.surfhip_ingest_create(C.byref(h), det.h, depth), "ingest_create")
+        self.handle = h.value
+
+    def acquire(self) -> np.ndarray:
+        p, pitch, stride = C.c_void_p(), C.c_int(), C.c_size_t()
+        check(_lib.surfhip_ingest_acquire(self.handle, C.byref(p), C.byref(pitch), C.byref(stride)),
+              "ingest_acquire")
+        n = self.det.max_batch * stride.value
+        buf = (C.c_uint8 * n).from_address(p.value)
+        return np.frombuffer(buf, np.uint8).reshape(self.det.max_batch, self.det.height, pitch.value)
+
+    def submit(self, nframes: int) -> None:
+        check(_lib.surfhip_ingest_submit(self.handle, nframes), "ingest_submit")
+
+    def collect(self, copy: bool = True) -> np.ndarray:
+        """copy=False returns a view of the pinned slab, valid until this
+        slot is collected again (`depth` collects later)."""
+        p, n = C.c_void_p(), C.c_size_t()
+        check(_lib.surfhip_ingest_collect(self.handle, C.byref(p), C.byref(n)), "ingest_collect")
+        v = np.frombuffer((C.c_uint8 * n.value).from_address(p.value), np.uint8)
+        return v.copy() if copy else v
+
+    def pending(self) -> int:
+        n = C.c_int()
+        check(_lib.surfhip_ingest_pending(self.handle, C.byref(n)), "ingest_pending")
+        return n.value
+
+    def close(self) -> None:
+        if self.handle:
+            check(_lib.surfhip_ingest_destroy(self.handle), "ingest_destroy")
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+DUMP_MAGIC = b"SURFKPD1"
+DUMP_HEADER_DTYPE = np.dtype([("magic", "S8"), ("header_bytes", "<u4"), ("version", "<u4"),
+                              ("width", "<u4"), ("height", "<u4"), ("nframes", "<u4"),
+                              ("nfeatures", "<u4"), ("total", "<u8"), ("slab_bytes", "<u8"),
+                              ("first_frame", "<u8"), ("thresh", "<f4"), ("noctaves", "u1"),
+                              ("upright", "u1"), ("extend", "u1"), ("doubled", "u1")])
+assert DUMP_HEADER_DTYPE.itemsize == 64
+
+
+def dump_append(path: str, slab: np.ndarray, width: int, height: int, param: SurfParam,
+                first_frame: int = 0) -> None:
+    """Append one result slab as a record of the keypoint file (surfhip_dump_append)."""
+    b = np.ascontiguousarray(slab, dtype=np.uint8)
+    check(_lib.surfhip_dump_append(path.encode(), b.ctypes.data, b.nbytes, width, height,
+                                   C.byref(param), first_frame), "dump_append")
+
+
+def read_dump(path: str):
+    """Records of a keypoint file: list of (header dict, counts, points, desc or None)."""
+    raw = np.fromfile(path, np.uint8)
+    out, o = [], 0
+    while o < raw.size:
+        if raw.size - o < 64:
+            raise ValueError(f"{path}: truncated record header at byte {o}")
+        h = raw[o:o + 64].view(DUMP_HEADER_DTYPE)[0]
+        if h["magic"] != DUMP_MAGIC or h["header_bytes"] != 64 or h["version"] != 1:
+            raise ValueError(f"{path}: bad record header at byte {o}")
+        n = int(h["slab_bytes"])
+        if raw.size - o - 64 < n:
+            raise ValueError(f"{path}: truncated slab at byte {o + 64}")
+        counts, pts, desc = parse_slab(raw[o + 64:o + 64 + n])
+        if len(counts) != h["nframes"] or len(pts) != h["total"]:
+            raise ValueError(f"{path}: record at byte {o} disagrees with its slab")
+        out.append(({k: (h[k].item() if k != "magic" else bytes(h[k])) for k in DUMP_HEADER_DTYPE.names},
+                    counts, pts, desc))
+        o += 64 + n
     return out
 
 

@@ -29,6 +29,8 @@ static_assert(offsetof(surfhip_point, o) == 12 && offsetof(surfhip_point, laplac
               offsetof(surfhip_point, ori) == 24 && offsetof(surfhip_point, ambiguity) == 44,
               "SurfPoint field offsets");
 
+static_assert(sizeof(surfhip_dump_header) == 64, "dump record header");
+
 static thread_local hipError_t g_last_hip = hipSuccess;
 
 #define HIPCHK(x)                                    \
@@ -740,6 +742,216 @@ int surfhip_match(surfhip_point* pts1, const surfhip_point* pts2, const float* f
     }
     HIPCHK(e);
     return SURFHIP_OK;
+}
+
+/* ------------------------------------------------------------- ingest --
+ * Pipelined host -> HBM -> result-slab ring.  The
+ * reference feeds one frame per call through a blocking cudaMemcpy2D of a
+ * pageable OpenCV buffer (main.cpp:212-226) and copies each frame's points
+ * back with a blocking cudaMemcpy (surf.cpp:335-342).  Here `depth` pinned
+ * host frame slots feed `depth` HBM frame slots over a copy stream; the
+ * detector stream waits only on its own slot's copy event, so batch i+1's
+ * PCIe transfer runs under batch i's kernels.  Each batch is packed into its
+ * slot's device slab right after describe (before the next batch may reuse
+ * the detector's scratch) and its 16-B header + counts come back
+ * asynchronously; collect() then copies exactly the slab's bytes to pinned
+ * host memory on a third stream while later batches keep computing. */
+struct surfhip_ingest {
+    surfhip_detector* det = nullptr;
+    int depth = 0, pitch = 0, hdr_bytes = 0;
+    size_t frame_bytes = 0, dslab_cap = 0;
+    hipStream_t copy = nullptr, out = nullptr;
+    uint8_t* h_frames[SURFHIP_INGEST_MAX_DEPTH]{};
+    uint8_t* d_frames[SURFHIP_INGEST_MAX_DEPTH]{};
+    uint8_t* d_slab[SURFHIP_INGEST_MAX_DEPTH]{};
+    int32_t* h_hdr[SURFHIP_INGEST_MAX_DEPTH]{};
+    uint8_t* h_slab[SURFHIP_INGEST_MAX_DEPTH]{};
+    size_t h_slab_cap[SURFHIP_INGEST_MAX_DEPTH]{};
+    int nframes[SURFHIP_INGEST_MAX_DEPTH]{};
+    hipEvent_t ev_h2d[SURFHIP_INGEST_MAX_DEPTH]{}, ev_done[SURFHIP_INGEST_MAX_DEPTH]{};
+    surfhip_point* d_pts = nullptr;
+    float* d_desc = nullptr;
+    int* d_counts = nullptr;
+    long long submitted = 0, collected = 0;
+    int acquired = -1;                  // slot handed out by acquire, not yet submitted
+};
+
+static void ingest_free(surfhip_ingest* g)
+{
+    for (int s = 0; s < SURFHIP_INGEST_MAX_DEPTH; ++s) {
+        if (g->h_frames[s]) (void)hipHostFree(g->h_frames[s]);
+        if (g->h_hdr[s]) (void)hipHostFree(g->h_hdr[s]);
+        if (g->h_slab[s]) (void)hipHostFree(g->h_slab[s]);
+        if (g->d_frames[s]) (void)hipFree(g->d_frames[s]);
+        if (g->d_slab[s]) (void)hipFree(g->d_slab[s]);
+        if (g->ev_h2d[s]) (void)hipEventDestroy(g->ev_h2d[s]);
+        if (g->ev_done[s]) (void)hipEventDestroy(g->ev_done[s]);
+    }
+    if (g->d_pts) (void)hipFree(g->d_pts);
+    if (g->d_desc) (void)hipFree(g->d_desc);
+    if (g->d_counts) (void)hipFree(g->d_counts);
+    if (g->copy) (void)hipStreamDestroy(g->copy);
+    if (g->out) (void)hipStreamDestroy(g->out);
+    delete g;
+}
+
+static int ingest_alloc(surfhip_ingest* g)
+{
+    surfhip_detector* d = g->det;
+    const int nf = d->param.nfeatures, B = d->max_batch;
+    g->pitch = (d->srcW + 127) & ~127;
+    g->frame_bytes = (size_t)g->pitch * d->srcH;
+    g->hdr_bytes = 16 + ((4 * B + 15) & ~15);
+    g->dslab_cap = surfhip_slab_bytes(B, B * d->max_pts, nf);
+    HIPCHK(hipStreamCreateWithFlags(&g->copy, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&g->out, hipStreamNonBlocking));
+    HIPCHK(hipMalloc(&g->d_pts, sizeof(surfhip_point) * (size_t)B * d->max_pts));
+    if (nf) HIPCHK(hipMalloc(&g->d_desc, sizeof(float) * (size_t)B * d->max_pts * nf));
+    HIPCHK(hipMalloc(&g->d_counts, sizeof(int) * (size_t)B));
+    for (int s = 0; s < g->depth; ++s) {
+        HIPCHK(hipHostMalloc(&g->h_frames[s], g->frame_bytes * B, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(&g->h_hdr[s], g->hdr_bytes, hipHostMallocDefault));
+        HIPCHK(hipMalloc(&g->d_frames[s], g->frame_bytes * B));
+        HIPCHK(hipMalloc(&g->d_slab[s], g->dslab_cap));
+        HIPCHK(hipEventCreateWithFlags(&g->ev_h2d[s], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&g->ev_done[s], hipEventDisableTiming));
+        memset(g->h_frames[s], 0, g->frame_bytes * B);
+    }
+    return SURFHIP_OK;
+}
+
+int surfhip_ingest_create(surfhip_ingest** out, surfhip_detector* det, int depth)
+{
+    if (!out || !det || depth < 1 || depth > SURFHIP_INGEST_MAX_DEPTH) return SURFHIP_ERR_INVALID;
+    *out = nullptr;
+    surfhip_ingest* g = new surfhip_ingest;
+    g->det = det;
+    g->depth = depth;
+    int rc = ingest_alloc(g);
+    if (rc != SURFHIP_OK) {
+        ingest_free(g);
+        return rc;
+    }
+    *out = g;
+    return SURFHIP_OK;
+}
+
+int surfhip_ingest_destroy(surfhip_ingest* g)
+{
+    if (!g) return SURFHIP_ERR_INVALID;
+    // wait on the ring's own events only: the detector may already be gone
+    hipError_t e = hipStreamSynchronize(g->copy);
+    for (long long b = g->collected; b < g->submitted; ++b) {
+        hipError_t e1 = hipEventSynchronize(g->ev_done[b % g->depth]);
+        if (e == hipSuccess) e = e1;
+    }
+    hipError_t e2 = hipStreamSynchronize(g->out);
+    ingest_free(g);
+    HIPCHK(e);
+    HIPCHK(e2);
+    return SURFHIP_OK;
+}
+
+int surfhip_ingest_acquire(surfhip_ingest* g, uint8_t** h_frames, int* pitch, size_t* frame_stride)
+{
+    if (!g || !h_frames) return SURFHIP_ERR_INVALID;
+    if (g->submitted - g->collected >= g->depth) return SURFHIP_ERR_CAPACITY;   // collect first
+    const int s = (int)(g->submitted % g->depth);
+    // the slot's previous batch was collected, so its copy and kernels are done
+    g->acquired = s;
+    *h_frames = g->h_frames[s];
+    if (pitch) *pitch = g->pitch;
+    if (frame_stride) *frame_stride = g->frame_bytes;
+    return SURFHIP_OK;
+}
+
+int surfhip_ingest_submit(surfhip_ingest* g, int nframes)
+{
+    if (!g || g->acquired < 0 || nframes < 1 || nframes > g->det->max_batch) return SURFHIP_ERR_INVALID;
+    surfhip_detector* d = g->det;
+    const int s = g->acquired;
+    g->acquired = -1;
+    g->nframes[s] = nframes;
+    HIPCHK(hipMemcpyAsync(g->d_frames[s], g->h_frames[s], g->frame_bytes * nframes, hipMemcpyHostToDevice,
+                          g->copy));
+    HIPCHK(hipEventRecord(g->ev_h2d[s], g->copy));
+    HIPCHK(hipStreamWaitEvent(d->stream, g->ev_h2d[s], 0));
+    int rc = surfhip_detect_batch(d, g->d_frames[s], nframes, g->pitch, g->frame_bytes, g->d_pts, g->d_desc,
+                                  g->d_counts);
+    if (rc != SURFHIP_OK) return rc;
+    rc = surfhip_pack_slab(d, g->d_pts, g->d_desc, g->d_counts, nframes, g->d_slab[s]);
+    if (rc != SURFHIP_OK) return rc;
+    HIPCHK(hipMemcpyAsync(g->h_hdr[s], g->d_slab[s], 16 + ((4 * nframes + 15) & ~15), hipMemcpyDeviceToHost,
+                          d->stream));
+    HIPCHK(hipEventRecord(g->ev_done[s], d->stream));
+    ++g->submitted;
+    return SURFHIP_OK;
+}
+
+int surfhip_ingest_collect(surfhip_ingest* g, const void** h_slab, size_t* bytes)
+{
+    if (!g || !h_slab || !bytes) return SURFHIP_ERR_INVALID;
+    if (g->collected >= g->submitted) return SURFHIP_ERR_INVALID;        // nothing in flight
+    const int s = (int)(g->collected % g->depth);
+    HIPCHK(hipEventSynchronize(g->ev_done[s]));
+    const int32_t* hdr = g->h_hdr[s];
+    if (hdr[0] != g->nframes[s] || hdr[1] < 0) return SURFHIP_ERR_HIP;
+    const size_t n = surfhip_slab_bytes(hdr[0], hdr[1], hdr[2]);
+    if (n > g->h_slab_cap[s]) {
+        if (g->h_slab[s]) HIPCHK(hipHostFree(g->h_slab[s]));
+        g->h_slab[s] = nullptr;
+        g->h_slab_cap[s] = 0;
+        const size_t cap = n + n / 4;
+        HIPCHK(hipHostMalloc(&g->h_slab[s], cap, hipHostMallocDefault));
+        g->h_slab_cap[s] = cap;
+    }
+    HIPCHK(hipMemcpyAsync(g->h_slab[s], g->d_slab[s], n, hipMemcpyDeviceToHost, g->out));
+    HIPCHK(hipStreamSynchronize(g->out));
+    ++g->collected;
+    *h_slab = g->h_slab[s];
+    *bytes = n;
+    return SURFHIP_OK;
+}
+
+int surfhip_ingest_pending(surfhip_ingest* g, int* n)
+{
+    if (!g || !n) return SURFHIP_ERR_INVALID;
+    *n = (int)(g->submitted - g->collected);
+    return SURFHIP_OK;
+}
+
+/* --------------------------------------------------------------- dump --
+ * Keypoint + descriptor file: a sequence of records, each a 64-B header
+ * followed by one result slab (the all-gather format above).  The reference
+ * has no on-disk format (it only draws keypoints, main.cpp:21-71). */
+int surfhip_dump_append(const char* path, const void* h_slab, size_t bytes, int width, int height,
+                        const surfhip_param* p, long long first_frame)
+{
+    if (!path || !h_slab || bytes < 16 || !p) return SURFHIP_ERR_INVALID;
+    const int32_t* sh = (const int32_t*)h_slab;
+    if (sh[0] < 0 || sh[1] < 0 || surfhip_slab_bytes(sh[0], sh[1], sh[2]) != bytes) return SURFHIP_ERR_INVALID;
+    surfhip_dump_header h;
+    memset(&h, 0, sizeof h);
+    memcpy(h.magic, SURFHIP_DUMP_MAGIC, 8);
+    h.header_bytes = sizeof h;
+    h.version = SURFHIP_DUMP_VERSION;
+    h.width = (uint32_t)width;
+    h.height = (uint32_t)height;
+    h.nframes = (uint32_t)sh[0];
+    h.nfeatures = (uint32_t)sh[2];
+    h.total = (uint64_t)sh[1];
+    h.slab_bytes = (uint64_t)bytes;
+    h.first_frame = (uint64_t)first_frame;
+    h.thresh = p->thresh;
+    h.noctaves = (uint8_t)p->noctaves;
+    h.upright = p->upright ? 1 : 0;
+    h.extend = p->extend ? 1 : 0;
+    h.doubled = p->doubled ? 1 : 0;
+    FILE* f = fopen(path, "ab");
+    if (!f) return SURFHIP_ERR_INVALID;
+    int ok = fwrite(&h, sizeof h, 1, f) == 1 && fwrite(h_slab, 1, bytes, f) == bytes;
+    ok = (fclose(f) == 0) && ok;
+    return ok ? SURFHIP_OK : SURFHIP_ERR_INVALID;
 }
 
 const char* surfhip_build_info(void)

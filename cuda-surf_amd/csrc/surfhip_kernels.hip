@@ -2657,7 +2657,8 @@ __global__ __launch_bounds__(256) void k_pack(const surfhip_point* __restrict__ 
     int* hdr = reinterpret_cast<int*>(slab);
     if (f == 0 && blockIdx.x == 0) {
         if (threadIdx.x == 0) { hdr[0] = nframes; hdr[1] = total; hdr[2] = desc ? nfeat : 0; hdr[3] = 0; }
-        for (int i = threadIdx.x; i < nframes; i += 256) hdr[4 + i] = counts[i];
+        const int npad = (nframes + 3) & ~3;          // counts padded to 16 B with zeros (stable file bytes)
+        for (int i = threadIdx.x; i < npad; i += 256) hdr[4 + i] = i < nframes ? counts[i] : 0;
     }
     const size_t head = 16 + (((size_t)nframes * 4 + 15) & ~(size_t)15);
     surfhip_point* pout = reinterpret_cast<surfhip_point*>(slab + head);

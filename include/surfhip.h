@@ -206,6 +206,50 @@ int surfhip_match(surfhip_point* d_pts1, const surfhip_point* d_pts2, const floa
                   const float* d_feat2, int n1, int n2, int nfeatures, int flags,
                   void* d_scratch, void* stream);
 
+/* ------------------------------------------------------------- ingest --
+ * Pipelined host-frame ingest.  Replaces the
+ * per-frame blocking cudaMemcpy2D of a pageable frame (main.cpp:212-226) and
+ * the blocking per-frame point copy-back (surf.cpp:335-342) with a ring of
+ * `depth` pinned host frame slots / HBM frame slots / result slabs:
+ *   acquire  -> pinned u8 slot [max_batch][H][pitch], pitch = align128(W)
+ *               (SURFHIP_ERR_CAPACITY when `depth` batches await collect)
+ *   submit   -> H2D on a copy stream, detect+describe on the detector's
+ *               stream after that copy only, pack into the slot's slab
+ *   collect  -> oldest batch's compacted result slab (format above) in
+ *               pinned host memory, valid until that slot is collected again
+ * Results are bit-identical to surfhip_detect_batch + surfhip_pack_slab. */
+#define SURFHIP_INGEST_MAX_DEPTH 8
+typedef struct surfhip_ingest surfhip_ingest;
+int surfhip_ingest_create(surfhip_ingest** ing, surfhip_detector* det, int depth);
+int surfhip_ingest_destroy(surfhip_ingest* ing);
+int surfhip_ingest_acquire(surfhip_ingest* ing, uint8_t** h_frames, int* pitch, size_t* frame_stride);
+int surfhip_ingest_submit(surfhip_ingest* ing, int nframes);
+int surfhip_ingest_collect(surfhip_ingest* ing, const void** h_slab, size_t* bytes);
+int surfhip_ingest_pending(surfhip_ingest* ing, int* n);
+
+/* --------------------------------------------------------------- dump --
+ * On-disk keypoint + descriptor file (no reference counterpart: main.cpp
+ * only draws the points, main.cpp:21-71).  A file is a sequence of records;
+ * a record is this 64-B little-endian header followed by slab_bytes of one
+ * result slab exactly as surfhip_pack_slab / surfhip_ingest_collect return
+ * it.  surfhip_dump_append appends one record (creating the file). */
+#define SURFHIP_DUMP_MAGIC "SURFKPD1"
+#define SURFHIP_DUMP_VERSION 1
+typedef struct surfhip_dump_header {
+    char     magic[8];              /* "SURFKPD1"                         */
+    uint32_t header_bytes;          /* 64                                 */
+    uint32_t version;               /* 1                                  */
+    uint32_t width, height;         /* frame size                         */
+    uint32_t nframes, nfeatures;    /* nfeatures 0: no descriptors        */
+    uint64_t total;                 /* keypoints in the slab              */
+    uint64_t slab_bytes;            /* bytes following this header       */
+    uint64_t first_frame;           /* caller's index of the first frame  */
+    float    thresh;
+    uint8_t  noctaves, upright, extend, doubled;
+} surfhip_dump_header;
+int surfhip_dump_append(const char* path, const void* h_slab, size_t bytes, int width, int height,
+                        const surfhip_param* param, long long first_frame);
+
 /* Library build identification (for the loaded-.so audit). */
 const char* surfhip_build_info(void);
 

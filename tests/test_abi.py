@@ -127,3 +127,44 @@ def test_shard_ranges(surf):
         assert sum(c for _, c in spans) == n
         for (s0, c0), (s1, _) in zip(spans, spans[1:]):
             assert s0 + c0 == s1
+
+
+def test_dump_file_roundtrip(surf, tmp_path):
+    """Keypoint file (surfhip_dump_append, host-only C): records of slabs
+    with and without descriptors read back byte-for-byte; bad input and a
+    truncated file are rejected."""
+    rng = np.random.default_rng(11)
+    path = str(tmp_path / "kp.surfkpd")
+    param = surf.make_param(4, 4.0, False, 9, 2, True, False, 4)
+    recs = []
+    for i, (nframes, nf) in enumerate(((3, 64), (1, 0), (4, 128), (2, 64))):
+        counts = rng.integers(0, 40, nframes).astype(np.int32)
+        counts[0] = 0                                           # an empty frame
+        total = int(counts.sum())
+        pts = np.zeros(total, surf.POINT_DTYPE)
+        pts["x"], pts["y"] = rng.random(total) * 1920, rng.random(total) * 1080
+        pts["laplace"] = rng.integers(0, 2, total)
+        desc = rng.random((total, nf)).astype(np.float32) if nf else None
+        slab = surf.build_slab(counts, pts, desc)
+        surf.dump_append(path, slab, 1920, 1080, param, first_frame=100 * i)
+        recs.append((counts, pts, desc))
+    back = surf.read_dump(path)
+    assert len(back) == len(recs)
+    for i, ((hdr, c, p, d), (c0, p0, d0)) in enumerate(zip(back, recs)):
+        assert hdr["magic"] == b"SURFKPD1" and hdr["width"] == 1920 and hdr["height"] == 1080
+        assert hdr["first_frame"] == 100 * i and hdr["upright"] == 1 and hdr["noctaves"] == 4
+        assert hdr["thresh"] == np.float32(4.0)
+        np.testing.assert_array_equal(c, c0)
+        assert p.tobytes() == p0.tobytes()
+        if d0 is None:
+            assert d is None and hdr["nfeatures"] == 0
+        else:
+            assert d.tobytes() == d0.tobytes()
+    good = surf.build_slab(np.array([2], np.int32), np.zeros(2, surf.POINT_DTYPE), None)
+    with pytest.raises(surf.SurfError):                          # slab size disagrees with its header
+        surf.dump_append(path, good[:-4], 64, 48, param)
+    raw = open(path, "rb").read()
+    bad = str(tmp_path / "trunc.surfkpd")
+    open(bad, "wb").write(raw[:-10])
+    with pytest.raises(ValueError):
+        surf.read_dump(bad)
