@@ -57,6 +57,16 @@ __device__ __forceinline__ unsigned lane_id()
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
+typedef float v2f32 __attribute__((ext_vector_type(2)));
+// 3 x mod 2^32 as one full-rate v_lshl_add_u32: LLVM lowers `3u * x` to
+// the quarter-rate v_mul_lo_u32 / v_mad_u64_u32, which made up about a
+// quarter of the Hessian kernels' VALU issue time
+__device__ __forceinline__ uint32_t mul3(uint32_t x)
+{
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, 1, %1" : "=v"(r) : "v"(x));
+    return r;
+}
 constexpr uint32_t kOOB = 0x80000000u;          // byte offset past every buffer here
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* base, long long bytes)
