@@ -1868,7 +1868,7 @@ __device__ __forceinline__ void place(float* d, int wsz, int osz, float mag1, in
 
 
 struct OriScratch {
-    int   hid[361];
+    uint64_t bmask[6][72];          // per 64-sample chunk and bin: member samples (bit = t % 64)
     float ang[361];
     float psum[361];
     int   hist[72];
@@ -1888,6 +1888,8 @@ __device__ float orientation_wave(const uint32_t* __restrict__ I, const FramePar
     const int pixsi = f2i_rz(2.f * scale + 1.6f);
     const int pixsi2 = f2i_rz(scale + 0.8f);
     const int ixo = f2i_rn(p.x), iyo = f2i_rn(p.y);
+    for (int t = lane; t < 6 * 72; t += 64) (&S.bmask[0][0])[t] = 0ull;
+    wave_sync();
     for (int t = lane; t < 361; t += 64) {
         const int y1 = t / 19 - 9, x1 = t % 19 - 9;
         const int xx = ixo + x1 * pixsi2, yy = iyo + y1 * pixsi2;
@@ -1906,17 +1908,22 @@ __device__ float orientation_wave(const uint32_t* __restrict__ I, const FramePar
                 }
             }
         }
-        S.hid[t] = hid;
         S.ang[t] = angle;
         S.psum[t] = psum;
+        if (hid >= 0) __hip_atomic_fetch_or(&S.bmask[t >> 6][hid], 1ull << (t & 63), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     wave_sync();
-    // per-bin sums in row-major sample order
+    // per-bin sums in row-major sample order (surfd.cu:1820-1840): a bin's
+    // lane walks only its member samples, chunk by chunk, bits ascending
     for (int b = lane; b < 72; b += 64) {
         int cnt = 0;
         float sa = 0.f, sp = 0.f, spa = 0.f, swrap = 0.f;
-        for (int t = 0; t < 361; t++) {
-            if (S.hid[t] == b) {
+        for (int c = 0; c < 6; c++) {
+            uint64_t m = S.bmask[c][b];
+            while (m) {
+                const int t = 64 * c + (int)__builtin_ctzll(m);
+                m &= m - 1;
                 const float a = S.ang[t], w = S.psum[t];
                 cnt += 1;
                 sa = sa + a;
@@ -1974,22 +1981,27 @@ __device__ float orientation_wave(const uint32_t* __restrict__ I, const FramePar
         S.was[i] = was;
     }
     wave_sync();
-    float ori = 0.f;
-    if (lane == 0) {
-        // tree argmax in chunks of 64 and 8, strict '<' (surfd.cu:1921-1947)
-        for (int stride = 32; stride > 0; stride >>= 1)
-            for (int t = 0; t < stride; t++)
-                if (S.ws[t] < S.ws[t + stride]) { S.ws[t] = S.ws[t + stride]; S.was[t] = S.was[t + stride]; }
-        for (int stride = 4; stride > 0; stride >>= 1)
-            for (int t = 0; t < stride; t++)
-                if (S.ws[64 + t] < S.ws[64 + t + stride]) { S.ws[64 + t] = S.ws[64 + t + stride]; S.was[64 + t] = S.was[64 + t + stride]; }
-        float w0 = S.ws[0], a0 = S.was[0];
-        if (w0 < S.ws[64]) { w0 = S.ws[64]; a0 = S.was[64]; }
-        ori = a0 / w0;
+    // tree argmax in chunks of 64 and 8, strict '<' (surfd.cu:1921-1947):
+    // level `stride` updates slots t < stride from t + stride, which that
+    // level never writes, so lane-parallel shuffles give the serial result
+    float w64 = S.ws[lane], a64 = S.was[lane];
+    const int l8 = (int)(lane & 7);
+    float w8 = S.ws[64 + l8], a8 = S.was[64 + l8];
+#pragma unroll
+    for (int stride = 32; stride > 0; stride >>= 1) {
+        const float wo = __shfl_down(w64, stride, 64), ao = __shfl_down(a64, stride, 64);
+        if ((int)lane < stride && w64 < wo) { w64 = wo; a64 = ao; }
     }
-    ori = __shfl(ori, 0, 64);
+#pragma unroll
+    for (int stride = 4; stride > 0; stride >>= 1) {
+        const float wo = __shfl_down(w8, stride, 64), ao = __shfl_down(a8, stride, 64);
+        if ((int)lane < stride && w8 < wo) { w8 = wo; a8 = ao; }
+    }
+    float w0 = __shfl(w64, 0, 64), a0 = __shfl(a64, 0, 64);
+    const float w1 = __shfl(w8, 0, 64), a1 = __shfl(a8, 0, 64);
+    if (w0 < w1) { w0 = w1; a0 = a1; }
     wave_sync();
-    return ori;
+    return a0 / w0;
 }
 
 template <bool UPRIGHT>
@@ -1998,7 +2010,12 @@ __global__ __launch_bounds__(256) void k_describe(const int32_t* __restrict__ ii
                                                   const int* __restrict__ counts, const int* __restrict__ offsets,
                                                   const int* __restrict__ order, int nframes, float* __restrict__ desc)
 {
-    __shared__ float sdesc[4][128];
+    // four copies of the descriptor per wave (copy = lane & 3, 132-float
+    // stride so that one bin's copies sit in different banks): neighbouring
+    // samples, which mostly hit the same cell and bin, no longer serialise
+    // on one LDS address; the copies are summed before normalisation
+    constexpr int DSTR = 132;
+    __shared__ float sdesc[4][4 * DSTR];
     __shared__ OriScratch sori[UPRIGHT ? 1 : 4];
     const unsigned lane = lane_id();
     const int w = threadIdx.x >> 6;
@@ -2006,7 +2023,8 @@ __global__ __launch_bounds__(256) void k_describe(const int32_t* __restrict__ ii
     const int nf = P.nfeat, wsz = P.wsz, osz = P.osz;
     const float fw = (float)wsz;
     const float wofs = (float)wsz * 0.5f - 0.5f;
-    float* d = sdesc[w];
+    float* const d0 = sdesc[w];
+    float* d = d0 + (lane & 3) * DSTR;
     for (int g = blockIdx.x * 4 + w; g < total; g += gridDim.x * 4) {
         int lo = 0, hi = nframes;            // offsets[lo] <= g < offsets[hi]
         while (hi - lo > 1) {
@@ -2023,7 +2041,7 @@ __global__ __launch_bounds__(256) void k_describe(const int32_t* __restrict__ ii
             ori = orientation_wave(I, P, p, sori[w], lane);
             if (lane == 0) pp->ori = ori;
         }
-        for (int t = lane; t < nf; t += 64) d[t] = 0.f;
+        for (int t = lane; t < 4 * DSTR; t += 64) d0[t] = 0.f;
         wave_sync();
         const float scale = 1.65f * p.scale;
         const int step = max(f2i_rn(scale * 0.5f), 1);
@@ -2087,8 +2105,9 @@ __global__ __launch_bounds__(256) void k_describe(const int32_t* __restrict__ ii
         }
         wave_sync();
         // normalize (surfd.cu:2447-2493): sequential-addressing tree
-        const float v0 = lane < (unsigned)nf ? d[lane] : 0.f;
-        const float v1 = (nf > 64 && lane + 64 < (unsigned)nf) ? d[lane + 64] : 0.f;
+        auto sum4 = [&](int b) { return ((d0[b] + d0[DSTR + b]) + d0[2 * DSTR + b]) + d0[3 * DSTR + b]; };
+        const float v0 = lane < (unsigned)nf ? sum4(lane) : 0.f;
+        const float v1 = (nf > 64 && lane + 64 < (unsigned)nf) ? sum4(lane + 64) : 0.f;
         float a = v0 * v0;
         if (nf > 64) a = a + v1 * v1;
 #pragma unroll
