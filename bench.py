@@ -244,6 +244,12 @@ def main():
         hb = det.hessian_bytes_per_frame() * B
         achieved = hb / (hess_ms * 1e-3) / 1e9
         traffic = pmc_traffic(args)
+        if (W, H) == (1920, 1080) and args.octaves == 4:
+            cfg_name = "config#3"
+        elif (W, H) == (3840, 2160) and args.octaves == 5 and not args.upright and args.extend:
+            cfg_name = "config#5"
+        else:
+            cfg_name = "custom"
         result = {
             "metric": METRIC if (W, H) == (1920, 1080) else f"{W}x{H} frames/sec (detect+describe)",
             "value": round(value, 2),
@@ -256,8 +262,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8/i32/f32",
-            "data": "synthetic (seeded Gaussian-blob 1080p frames, resident in HBM)",
-            "config": {"workload": f"config#3 batch {B} x {W}x{H} per GPU, {args.octaves} octaves, "
+            "data": f"synthetic (seeded Gaussian-blob {W}x{H} frames, resident in HBM)",
+            "config": {"workload": f"{cfg_name} batch {B} x {W}x{H} per GPU, {args.octaves} octaves, "
                                    f"{nf}-D {'upright' if args.upright else 'rotated'} descriptors, thresh {args.thresh}"
                                    + (", RCCL all-gather of compacted SurfPoint+descriptor slabs" if world > 1 else ""),
                        "frames_per_gpu_per_step": B, "width": W, "height": H, "octaves": args.octaves,
