@@ -860,6 +860,7 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
     plan.o0_nbx = (oct[0].sw + o0::TXS - 1) / o0::TXS;     // strips per frame
     plan.o0_blocks = plan.o0_nbx;
     plan.o0_v = plan.o0_lds && getenv("SURFHIP_O0_RING") == nullptr;   // A/B switch back to k_hess_o0
+    plan.o0_split = getenv("SURFHIP_V0_SPLIT") ? atoi(getenv("SURFHIP_V0_SPLIT")) : 0;   // k_hess_v0 scale groups
     plan.o0_vstrips = (oct[0].sw + 63) / 64;
     plan.o1_lds = P.noct > 1 && o1_lds_ok(P, oct[1]);
     plan.o1_v = plan.o1_lds && getenv("SURFHIP_O1_RING") == nullptr;   // A/B switch back to k_hess_o1
@@ -1165,8 +1166,24 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
     if (plan.o0_v && frames) {
         if (u8p) {
         const int per_xcd = (nf8 / 8) * plan.o0_vstrips;           // wave tasks per XCD
-        k_hess_v0<4, 1, 0x1f><<<dim3(8 * ((per_xcd + v0::WAVES - 1) / v0::WAVES)), v0::THREADS, 0, s>>>(
-            frames, pitch, fstride, resp, P, h_oct[0], plan.o0_vstrips, nframes);
+        const dim3 g(8 * ((per_xcd + v0::WAVES - 1) / v0::WAVES));
+        const int split = plan.o0_split;
+        if (split == 1) {           // scales 0-2 and 3-4 in two launches (fewer live accumulators)
+            k_hess_v0<4, 1, 0x07><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
+                                                            plan.o0_vstrips, nframes);
+            k_hess_v0<4, 1, 0x18><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
+                                                            plan.o0_vstrips, nframes);
+        } else if (split == 2) {    // scales 0-1, 2-3, 4
+            k_hess_v0<4, 1, 0x03><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
+                                                            plan.o0_vstrips, nframes);
+            k_hess_v0<4, 1, 0x0c><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
+                                                            plan.o0_vstrips, nframes);
+            k_hess_v0<4, 1, 0x10><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
+                                                            plan.o0_vstrips, nframes);
+        } else {
+            k_hess_v0<4, 1, 0x1f><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
+                                                            plan.o0_vstrips, nframes);
+        }
         }
     } else if (plan.o0_lds && iip)
         k_hess_o0<<<dim3(nf8 * plan.o0_nbx), o0::THREADS, 0, s>>>(ii, resp, P, h_oct[0], plan.o0_nbx, nframes);

@@ -120,13 +120,15 @@ def test_hessian_planes_bit_exact(surf, orc, w, h, noct):
         assert same.all(), f"octave {o} scale {s}: {(~same).sum()} cells differ, first at {np.argwhere(~same)[0]}"
 
 
-@pytest.mark.parametrize("env", ["SURFHIP_O0_RING", "SURFHIP_O1_RING", "SURFHIP_FAR_V"])
+@pytest.mark.parametrize("env", ["SURFHIP_O0_RING", "SURFHIP_O1_RING", "SURFHIP_FAR_V", "SURFHIP_V0_SPLIT=1",
+                                 "SURFHIP_V0_SPLIT=2"])
 @pytest.mark.parametrize("w,h,noct", [(640, 480, 4), (1920, 1080, 4)])
 def test_hessian_alternate_kernels_bit_exact(surf, orc, monkeypatch, env, w, h, noct):
     """The selectable Hessian kernels (integral-image rings for octaves 0/1,
     the u8 vertical-streaming kernel for octaves 2/3) give the same planes;
     the plan reads these switches when a detector is created."""
-    monkeypatch.setenv(env, "1")
+    name, _, val = env.partition("=")
+    monkeypatch.setenv(name, val or "1")
     frames = surf.synth_frames(1, w, h, first=21)
     param = surf.make_param(noct, 4.0, upright=True)
     res = gpu_run(surf, param, frames, w, h, want_ws=True, desc=False)
