@@ -2139,6 +2139,186 @@ __global__ __launch_bounds__(256) void k_describe(const int32_t* __restrict__ ii
 }
 
 // ----------------------------------------------------------------------
+// Rotated descriptor without atomics (wsz = 4; 64-D or 128-D extended).
+// The rotated window's sample grid (surfd.cu:2391-2444) is not separable,
+// but each sample adds only into the 2 x 2 cells at its floor cell (ri, ci)
+// (placeInIndex, surfd.cu:1199-1271).  So a lane pair owns one floor cell
+// of the 5 x 5 set {-1..3}^2: it walks the grid samples inside a
+// conservative bounding box of that cell's rotated square (the inverse
+// rotation of its corners, one sample of slack), keeps exactly the samples
+// whose floor cell -- computed with the reference's float ops -- is its own
+// (so every sample is counted once), and accumulates the 4 cells x NB bins
+// it can touch in registers.  A fixed-order sum over the (at most 8)
+// contributing lanes of each output bin replaces the LDS float atomics,
+// so the descriptor is deterministic.  Orientation as k_describe.
+// ----------------------------------------------------------------------
+struct RotScratch {
+    union {
+        OriScratch ori;
+        float red[64][4 * 8 + 1];   // per lane: 4 relative cells x NB bins (+1 pad)
+    };
+};
+
+template <int NB>
+__global__ __launch_bounds__(256) void k_describe_rot(const int32_t* __restrict__ ii, FrameParams P,
+                                                      surfhip_point* __restrict__ pts, int max_pts,
+                                                      const int* __restrict__ offsets, const int* __restrict__ order,
+                                                      int nframes, float* __restrict__ desc)
+{
+    constexpr int WSZ = 4, NC = WSZ + 1, NF = WSZ * WSZ * NB;
+    __shared__ RotScratch sr[4];
+    const unsigned lane = lane_id();
+    const int w = threadIdx.x >> 6;
+    const int total = offsets[nframes];
+    const float fw = (float)WSZ;
+    const float wofs = (float)WSZ * 0.5f - 0.5f;
+    // this lane's floor cell (lanes 50..63 own none)
+    const int cidx = (int)lane >> 1, half = (int)lane & 1;
+    const bool owner = cidx < NC * NC;
+    const int cri = owner ? cidx / NC - 1 : -100, cci = owner ? cidx % NC - 1 : -100;
+    RotScratch& S = sr[w];
+    for (int g = blockIdx.x * 4 + w; g < total; g += gridDim.x * 4) {
+        int lo = 0, hi = nframes;            // offsets[lo] <= g < offsets[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (offsets[mid] <= g) lo = mid; else hi = mid;
+        }
+        const int f = lo, i = order[(size_t)lo * max_pts + (g - offsets[lo])];
+        surfhip_point* pp = pts + (size_t)f * max_pts + i;
+        const surfhip_point p = *pp;
+        const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
+        const int ip = P.ip;
+        const float ori = orientation_wave(I, P, p, S.ori, lane);
+        if (lane == 0) pp->ori = ori;
+
+        const float scale = 1.65f * p.scale;
+        const int step = max(f2i_rn(scale * 0.5f), 1);
+        const int ix = f2i_rn(p.x), iy = f2i_rn(p.y);
+        const float spacing = scale * (float)P.mag;
+        const int hs = f2i_rz(scale);
+        const int rlim = P.iH - 1 - hs, clim = P.W - hs;
+        const float fracx = p.x - (float)ix, fracy = p.y - (float)iy;
+        const float sine = sincos_poly(ori, 0), cose = sincos_poly(ori, 1);
+        const float fracc = ((-sine) * fracy) + (cose * fracx);
+        const float fracr = (cose * fracy) + (sine * fracx);
+        const int iradius = f2i_rn((((1.4f * spacing) * (float)(WSZ + 1)) * 0.5f) / (float)step);
+        const float fstep = (float)step;
+        // grid box of this lane's cell: inverse rotation of its corners
+        int i0 = 1, i1 = 0, j0 = 0, j1 = 0;
+        if (owner) {
+            float mni = 1e30f, mxi = -1e30f, mnj = 1e30f, mxj = -1e30f;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const float A = ((float)(cri + (k >> 1)) - wofs) * spacing + fracr;
+                const float B = ((float)(cci + (k & 1)) - wofs) * spacing + fracc;
+                const float fi = (cose * A - sine * B) / fstep, fj = (sine * A + cose * B) / fstep;
+                mni = fminf(mni, fi); mxi = fmaxf(mxi, fi);
+                mnj = fminf(mnj, fj); mxj = fmaxf(mxj, fj);
+            }
+            i0 = max(-iradius, (int)floorf(mni) - 1);
+            i1 = min(iradius, (int)ceilf(mxi) + 1);
+            j0 = max(-iradius, (int)floorf(mnj) - 1);
+            j1 = min(iradius, (int)ceilf(mxj) + 1);
+            i0 += half;                      // the pair splits the box rows by parity
+        }
+        const int nj = j1 - j0 + 1;
+        const int nrows = i1 >= i0 ? (i1 - i0) / 2 + 1 : 0;
+        const int ncand = nj > 0 ? nrows * nj : 0;
+        float acc[4][NB];
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+            for (int b = 0; b < NB; b++) acc[q][b] = 0.f;
+        int si = i0, sj = j0;
+        for (int t = 0; t < ncand; t++, sj++) {
+            if (sj > j1) { sj = j0; si += 2; }
+            const float fi = (float)si, fj = (float)sj;
+            const float rpos = ((fstep * ((cose * fi) + (sine * fj))) - fracr) / spacing;
+            const float cpos = ((fstep * (((-sine) * fi) + (cose * fj))) - fracc) / spacing;
+            const float rx = rpos + wofs, cx = cpos + wofs;
+            if (!(rx > -1.f && rx < fw && cx > -1.f && cx < fw)) continue;
+            const int ri = f2i_rz(rx >= 0.f ? rx : rx - 1.f);
+            const int ci = f2i_rz(cx >= 0.f ? cx : cx - 1.f);
+            if (ri != cri || ci != cci) continue;
+            const int r = iy + si * step, c = ix + sj * step;
+            if (!(r >= 1 + hs && r < rlim && c >= 1 + hs && c < clim)) continue;
+            const float weight = c_tab.lut2[f2i_rz(rpos * rpos + cpos * cpos)];
+            const float dxx = (weight * (float)wavelet2(I, ip, c, r, hs)) * INV255;
+            const float dyy = (weight * (float)wavelet1(I, ip, c, r, hs)) * INV255;
+            const float dx = (cose * dxx) + (sine * dyy);
+            const float dy = (sine * dxx) - (cose * dyy);
+            const float rfrac = rx - (float)ri, cfrac = cx - (float)ci;
+            const float cfrac1 = 1 - cfrac;
+            // placeInIndex products (surfd.cu:1222-1266): cell weight by row, then column
+            // one placeInIndex value: bin BN when `neg`, else BP (both static)
+            auto put = [&](auto bn, auto bp, float mag, bool neg) {
+                constexpr int BN = decltype(bn)::value, BP = decltype(bp)::value;
+                const float r0 = mag * (1.f - rfrac), r1 = mag * rfrac;
+                const float v[4] = {r0 * cfrac1, r0 * cfrac, r1 * cfrac1, r1 * cfrac};
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    acc[q][BN] += neg ? v[q] : 0.f;
+                    acc[q][BP] += neg ? 0.f : v[q];
+                }
+            };
+            using I0 = std::integral_constant<int, 0>;
+            using I1 = std::integral_constant<int, 1>;
+            using I2 = std::integral_constant<int, 2>;
+            using I3 = std::integral_constant<int, 3>;
+            if constexpr (NB == 4) {
+                put(I0{}, I1{}, dx, dx < 0);
+                put(I2{}, I3{}, dy, dy < 0);
+            } else {
+                using I4 = std::integral_constant<int, 4>;
+                using I5 = std::integral_constant<int, 5>;
+                using I6 = std::integral_constant<int, 6>;
+                using I7 = std::integral_constant<int, 7>;
+                put(I0{}, I1{}, dx, dy < 0);
+                put(I2{}, I3{}, fabsf(dx), dy < 0);
+                put(I4{}, I5{}, dy, dx < 0);
+                put(I6{}, I7{}, fabsf(dy), dx < 0);
+            }
+        }
+        wave_sync();                          // orientation scratch is dead: reuse it
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+            for (int b = 0; b < NB; b++) S.red[lane][q * NB + b] = acc[q][b];
+        wave_sync();
+        // output bin (R, C, b): floor cells (R, C), (R, C-1), (R-1, C), (R-1, C-1)
+        // via relative cells 0..3, each by its two lanes, in that fixed order
+        float vout[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int o = (int)lane + 64 * h;
+            float a = 0.f;
+            if (o < NF) {
+                const int cell = o / NB, b = o % NB, R = cell / WSZ, C = cell % WSZ;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int fr = R - (q >> 1), fc = C - (q & 1);      // floor cell of the contributors
+                    const int fl = ((fr + 1) * NC + (fc + 1)) * 2;
+                    a = a + S.red[fl][q * NB + b];
+                    a = a + S.red[fl + 1][q * NB + b];
+                }
+            }
+            vout[h] = a;
+        }
+        // normalize (surfd.cu:2447-2493)
+        float a2 = vout[0] * vout[0];
+        if (NF > 64) a2 = a2 + vout[1] * vout[1];
+#pragma unroll
+        for (int k = 32; k >= 1; k >>= 1) a2 = a2 + __shfl_down(a2, k, 64);
+        const float tot = __shfl(a2, 0, 64);
+        const float fac = 1.f / sqrtf(tot);
+        float* out = desc + ((size_t)f * max_pts + i) * NF;
+        out[lane] = vout[0] * fac;
+        if (NF > 64) out[lane + 64] = vout[1] * fac;
+        wave_sync();
+    }
+}
+
+// ----------------------------------------------------------------------
 // Upright descriptor (U-SURF, 4x4 cells), deterministic and atomic-free.
 // The upright sample grid is separable (surfd.cu:1290-1294): a sample's cell
 // row (ri, rfrac) depends only on its grid row i, its cell column (ci, cfrac)
@@ -2680,6 +2860,9 @@ hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_poin
         else k_describe_ur<false><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc);
     } else if (P.upright) {
         k_describe<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, counts, offsets, order, nframes, desc);
+    } else if (P.wsz == 4 && getenv("SURFHIP_ROT_ATOMIC") == nullptr) {
+        if (P.osz == 8) k_describe_rot<8><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc);
+        else k_describe_rot<4><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc);
     } else {
         k_describe<false><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, counts, offsets, order, nframes, desc);
     }

@@ -153,6 +153,29 @@ def test_detect_describe_synthetic(surf, orc, upright, extend):
         compare_frame(res["pts"][f], res["desc"][f], o_pts, o_desc, upright)
 
 
+@pytest.mark.parametrize("extend", [False, True])
+@pytest.mark.parametrize("atomic", [False, True])
+def test_rotated_descriptor_kernels(surf, orc, monkeypatch, extend, atomic):
+    """Rotated 4x4 descriptors: the atomic-free floor-cell kernel (default,
+    k_describe_rot) and the LDS-atomic kernel (SURFHIP_ROT_ATOMIC) against the
+    oracle; the atomic-free one is also run twice and must repeat bit for bit."""
+    if atomic:
+        monkeypatch.setenv("SURFHIP_ROT_ATOMIC", "1")
+    w, h = 1280, 720
+    frames = surf.synth_frames(2, w, h, first=300)
+    param = surf.make_param(5, 4.0, upright=False, extend=extend)
+    res = gpu_run(surf, param, frames, w, h)
+    op = orc.make_param(5, 4.0, upright=False, extend=extend)
+    for f in range(2):
+        o_pts, o_desc, _ = orc.detect(op, frames[f], w, h)
+        assert len(o_pts) > 100
+        compare_frame(res["pts"][f], res["desc"][f], o_pts, o_desc, False)
+    if not atomic:
+        again = gpu_run(surf, param, frames, w, h)
+        for f in range(2):
+            assert again["desc"][f].tobytes() == res["desc"][f].tobytes()
+
+
 @pytest.mark.parametrize("index", [0, 56])
 def test_detect_describe_1080p(surf, orc, index):
     """Config #2: single 1920x1080, 4 octaves, 64-D, upright (main.cpp:187-204).
