@@ -2221,18 +2221,49 @@ __global__ __launch_bounds__(256) void k_describe_rot(const int32_t* __restrict_
             j1 = min(iradius, (int)ceilf(mxj) + 1);
             i0 += half;                      // the pair splits the box rows by parity
         }
-        const int nj = j1 - j0 + 1;
-        const int nrows = i1 >= i0 ? (i1 - i0) / 2 + 1 : 0;
-        const int ncand = nj > 0 ? nrows * nj : 0;
+        // per box row, the sj interval where the cell's two slabs (rx in
+        // [cri, cri + 1], cx in [cci, cci + 1]) cross the row, one sample of
+        // slack each side; a near-zero slope keeps the whole box row
+        const float Alo = (((float)cri - wofs) * spacing + fracr) / fstep;
+        const float Ahi = (((float)(cri + 1) - wofs) * spacing + fracr) / fstep;
+        const float Blo = (((float)cci - wofs) * spacing + fracc) / fstep;
+        const float Bhi = (((float)(cci + 1) - wofs) * spacing + fracc) / fstep;
+        const bool use_s = fabsf(sine) > 1e-3f, use_c = fabsf(cose) > 1e-3f;
+        const float inv_s = use_s ? 1.f / sine : 0.f, inv_c = use_c ? 1.f / cose : 0.f;
+        int rlo = 0, rhi = -1;
+        auto row_range = [&](int row) {
+            const float fi = (float)row;
+            float lo = (float)j0, hi = (float)j1;
+            if (use_s) {                     // sine * fj in [Alo - cose fi, Ahi - cose fi]
+                const float a = (Alo - cose * fi) * inv_s, b = (Ahi - cose * fi) * inv_s;
+                lo = fmaxf(lo, fminf(a, b) - 1.f);
+                hi = fminf(hi, fmaxf(a, b) + 1.f);
+            }
+            if (use_c) {                     // cose * fj in [Blo + sine fi, Bhi + sine fi]
+                const float a = (Blo + sine * fi) * inv_c, b = (Bhi + sine * fi) * inv_c;
+                lo = fmaxf(lo, fminf(a, b) - 1.f);
+                hi = fminf(hi, fmaxf(a, b) + 1.f);
+            }
+            rlo = (int)floorf(lo);
+            rhi = (int)ceilf(hi);
+            rlo = max(rlo, j0);
+            rhi = min(rhi, j1);
+        };
         float acc[4][NB];
 #pragma unroll
         for (int q = 0; q < 4; q++)
 #pragma unroll
             for (int b = 0; b < NB; b++) acc[q][b] = 0.f;
-        int si = i0, sj = j0;
-        for (int t = 0; t < ncand; t++, sj++) {
-            if (sj > j1) { sj = j0; si += 2; }
-            const float fi = (float)si, fj = (float)sj;
+        int si = i0, sj = 0;
+        if (si <= i1) { row_range(si); sj = rlo; }
+        while (si <= i1) {
+            if (sj > rhi) {
+                si += 2;
+                if (si <= i1) { row_range(si); sj = rlo; }
+                continue;
+            }
+            const int cj = sj++;
+            const float fi = (float)si, fj = (float)cj;
             const float rpos = ((fstep * ((cose * fi) + (sine * fj))) - fracr) / spacing;
             const float cpos = ((fstep * (((-sine) * fi) + (cose * fj))) - fracc) / spacing;
             const float rx = rpos + wofs, cx = cpos + wofs;
@@ -2240,7 +2271,7 @@ __global__ __launch_bounds__(256) void k_describe_rot(const int32_t* __restrict_
             const int ri = f2i_rz(rx >= 0.f ? rx : rx - 1.f);
             const int ci = f2i_rz(cx >= 0.f ? cx : cx - 1.f);
             if (ri != cri || ci != cci) continue;
-            const int r = iy + si * step, c = ix + sj * step;
+            const int r = iy + si * step, c = ix + cj * step;
             if (!(r >= 1 + hs && r < rlim && c >= 1 + hs && c < clim)) continue;
             const float weight = c_tab.lut2[f2i_rz(rpos * rpos + cpos * cpos)];
             const float dxx = (weight * (float)wavelet2(I, ip, c, r, hs)) * INV255;
