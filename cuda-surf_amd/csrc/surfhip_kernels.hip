@@ -2222,8 +2222,11 @@ __global__ __launch_bounds__(256) void k_describe_rot(const int32_t* __restrict_
             i0 += half;                      // the pair splits the box rows by parity
         }
         // per box row, the sj interval where the cell's two slabs (rx in
-        // [cri, cri + 1], cx in [cci, cci + 1]) cross the row, one sample of
-        // slack each side; a near-zero slope keeps the whole box row
+        // [cri, cri + 1], cx in [cci, cci + 1]) cross the row, widened by
+        // kSlack samples (the inverse's float error is < 1e-2 samples for
+        // slopes >= 1e-3; membership itself is the exact test below); a
+        // near-zero slope keeps the whole box row
+        constexpr float kSlack = 0.05f;
         const float Alo = (((float)cri - wofs) * spacing + fracr) / fstep;
         const float Ahi = (((float)(cri + 1) - wofs) * spacing + fracr) / fstep;
         const float Blo = (((float)cci - wofs) * spacing + fracc) / fstep;
@@ -2236,13 +2239,13 @@ __global__ __launch_bounds__(256) void k_describe_rot(const int32_t* __restrict_
             float lo = (float)j0, hi = (float)j1;
             if (use_s) {                     // sine * fj in [Alo - cose fi, Ahi - cose fi]
                 const float a = (Alo - cose * fi) * inv_s, b = (Ahi - cose * fi) * inv_s;
-                lo = fmaxf(lo, fminf(a, b) - 1.f);
-                hi = fminf(hi, fmaxf(a, b) + 1.f);
+                lo = fmaxf(lo, fminf(a, b) - kSlack);
+                hi = fminf(hi, fmaxf(a, b) + kSlack);
             }
             if (use_c) {                     // cose * fj in [Blo + sine fi, Bhi + sine fi]
                 const float a = (Blo + sine * fi) * inv_c, b = (Bhi + sine * fi) * inv_c;
-                lo = fmaxf(lo, fminf(a, b) - 1.f);
-                hi = fminf(hi, fmaxf(a, b) + 1.f);
+                lo = fmaxf(lo, fminf(a, b) - kSlack);
+                hi = fminf(hi, fmaxf(a, b) + kSlack);
             }
             rlo = (int)floorf(lo);
             rhi = (int)ceilf(hi);
