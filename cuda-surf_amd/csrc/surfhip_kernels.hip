@@ -1886,8 +1886,7 @@ __device__ __forceinline__ void place(float* d, int wsz, int osz, float mag1, in
 
 struct OriScratch {
     uint64_t bmask[6][72];          // per 64-sample chunk and bin: member samples (bit = t % 64)
-    float ang[361];
-    float psum[361];
+    float2 ap[361];                 // (angle, weighted magnitude) per sample: one ds_read_b64
     int   hist[72];
     float avg[72];
     float part[72];
@@ -1925,8 +1924,7 @@ __device__ float orientation_wave(const uint32_t* __restrict__ I, const FramePar
                 }
             }
         }
-        S.ang[t] = angle;
-        S.psum[t] = psum;
+        S.ap[t] = make_float2(angle, psum);
         if (hid >= 0) __hip_atomic_fetch_or(&S.bmask[t >> 6][hid], 1ull << (t & 63), __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_WORKGROUP);
     }
@@ -1941,7 +1939,8 @@ __device__ float orientation_wave(const uint32_t* __restrict__ I, const FramePar
             while (m) {
                 const int t = 64 * c + (int)__builtin_ctzll(m);
                 m &= m - 1;
-                const float a = S.ang[t], w = S.psum[t];
+                const float2 apt = S.ap[t];
+                const float a = apt.x, w = apt.y;
                 cnt += 1;
                 sa = sa + a;
                 sp = sp + w;
