@@ -423,14 +423,16 @@ def test_doubled_reference_image(surf, orc):
     compare_frame(res["pts"][0], res["desc"][0], o_pts, o_desc, True)
 
 
-@pytest.mark.parametrize("depth", [1, 2, 3])
-def test_ingest_ring_equals_resident_batches(surf, depth, tmp_path):
+@pytest.mark.parametrize("depth,upright,extend", [(1, True, False), (2, True, False), (3, True, False),
+                                                  (2, False, True)])
+def test_ingest_ring_equals_resident_batches(surf, depth, upright, extend, tmp_path):
     """Pinned-host ingest ring (surfhip_ingest_*): five batches (last one
     ragged) through a ring of `depth` slots give slabs byte-identical to
     detect_batch + pack_slab on the same frames resident in HBM; the
     keypoint file written from them reads back the same."""
     w, h, B, max_pts = 320, 240, 3, 4096
-    param = surf.make_param(4, 4.0, False, 9, 2, True, False, 4)
+    param = surf.make_param(4, 4.0, False, 9, 2, upright, extend, 4)
+    nf = param.nfeatures
     sizes = [3, 3, 2, 3, 1]
     frames = surf.synth_frames(sum(sizes), w, h, first=40)
     n_all, _, pitch = frames.shape
@@ -438,7 +440,7 @@ def test_ingest_ring_equals_resident_batches(surf, depth, tmp_path):
     ref = []
     det = surf.Detector(param, w, h, max_batch=B, max_pts=max_pts)
     fb, pb = surf.DeviceBuffer(frames[:B].nbytes), surf.DeviceBuffer(48 * B * max_pts)
-    db, cb = surf.DeviceBuffer(4 * B * max_pts * 64), surf.DeviceBuffer(4 * B)
+    db, cb = surf.DeviceBuffer(4 * B * max_pts * nf), surf.DeviceBuffer(4 * B)
     first = 0
     for n in sizes:
         fb.upload(np.ascontiguousarray(frames[first:first + n]))
