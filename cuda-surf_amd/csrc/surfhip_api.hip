@@ -440,7 +440,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
         e = hipMalloc((void**)&(ptr), (bytes));              \
         if (e != hipSuccess) goto fail;                      \
     } while (0)
-    make_plan(d->P, d->oct, d->plan, d->far);
+    make_plan(d->P, d->oct, d->plan, d->far, max_batch);
     ALLOC(d->d_oct, sizeof(OctaveParams) * kMaxOct);
     ALLOC(d->ii, B * d->P.ii_stride * sizeof(int32_t));
     ALLOC(d->resp, B * d->tot_osize * sizeof(float));

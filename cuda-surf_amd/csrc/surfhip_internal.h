@@ -92,7 +92,11 @@ struct FarPlan {
     int H, nstrips, nsteps, lds_bytes, acc_total;
     FarOct oc[farc::MAXO];
 };
-void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, FarPlan& far);
+// max_batch <= kGatherBatch (or SURFHIP_HESS_GATHER=1; =0 disables) puts every
+// octave on the one-thread-per-response gather kernel: the streaming kernels
+// walk whole strips, one wave each, too few waves to fill the chip for 1-2 frames.
+constexpr int kGatherBatch = 2;
+void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, FarPlan& far, int max_batch);
 
 // frames may be null (no u8 source known): every octave then reads the integral image
 hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, const int32_t* ii, float* resp,

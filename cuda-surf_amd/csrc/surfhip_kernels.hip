@@ -846,23 +846,26 @@ static bool vfar_ok(const FrameParams& P, const OctaveParams& q, int o)
     return true;
 }
 
-void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, FarPlan& far)
+void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, FarPlan& far, int max_batch)
 {
     int hb = 0, nb = 0;
+    const char* ge = getenv("SURFHIP_HESS_GATHER");
+    const bool gather = ge ? atoi(ge) != 0 : max_batch <= kGatherBatch;
     // k_hess_vfar (u8, 0.45 + 0.76 ms/batch for octaves 2 / 3) loses to the
     // integral-image LDS kernel k_hess_far (1.03 ms for both) for now: opt-in
     const bool use_vfar = getenv("SURFHIP_FAR_V") != nullptr;
     plan.vfar_n = 0;
     for (int o = 2; use_vfar && o < P.noct && o < 4 && vfar_ok(P, oct[o], o); o++) plan.vfar_n = o - 1;
-    if (plan.vfar_n > 0) far = FarPlan{};
+    if (plan.vfar_n > 0 || gather) far = FarPlan{};
     else make_far_plan(P, oct, far);
-    plan.o0_lds = P.noct > 0 && o0_lds_ok(P, oct[0]);
+    if (gather) plan.vfar_n = 0;
+    plan.o0_lds = !gather && P.noct > 0 && o0_lds_ok(P, oct[0]);
     plan.o0_nbx = (oct[0].sw + o0::TXS - 1) / o0::TXS;     // strips per frame
     plan.o0_blocks = plan.o0_nbx;
     plan.o0_v = plan.o0_lds && getenv("SURFHIP_O0_RING") == nullptr;   // A/B switch back to k_hess_o0
     plan.o0_split = getenv("SURFHIP_V0_SPLIT") ? atoi(getenv("SURFHIP_V0_SPLIT")) : 0;   // k_hess_v0 scale groups
     plan.o0_vstrips = (oct[0].sw + 63) / 64;
-    plan.o1_lds = P.noct > 1 && o1_lds_ok(P, oct[1]);
+    plan.o1_lds = !gather && P.noct > 1 && o1_lds_ok(P, oct[1]);
     plan.o1_v = plan.o1_lds && getenv("SURFHIP_O1_RING") == nullptr;   // A/B switch back to k_hess_o1
     plan.o1_vstrips = P.noct > 1 ? (oct[1].sw + 63) / 64 : 0;
     plan.o1_nbx = P.noct > 1 ? (oct[1].sw + o1::TXS - 1) / o1::TXS : 0;

@@ -16,6 +16,12 @@ import sys
 import numpy as np
 import pytest
 
+
+# The parity tests run small batches; keep them on the streaming Hessian
+# kernels the batched path uses (a detector with max_batch <= 2 would pick the
+# gather kernel); tests of the gather plan set SURFHIP_HESS_GATHER=1 themselves.
+os.environ.setdefault("SURFHIP_HESS_GATHER", "0")
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(REPO, "tests", "golden")
 REF_DATA = "/root/reference/data"       # present in the build container only

@@ -121,7 +121,7 @@ def test_hessian_planes_bit_exact(surf, orc, w, h, noct):
 
 
 @pytest.mark.parametrize("env", ["SURFHIP_O0_RING", "SURFHIP_O1_RING", "SURFHIP_FAR_V", "SURFHIP_V0_SPLIT=1",
-                                 "SURFHIP_V0_SPLIT=2"])
+                                 "SURFHIP_V0_SPLIT=2", "SURFHIP_HESS_GATHER=1"])
 @pytest.mark.parametrize("w,h,noct", [(640, 480, 4), (1920, 1080, 4)])
 def test_hessian_alternate_kernels_bit_exact(surf, orc, monkeypatch, env, w, h, noct):
     """The selectable Hessian kernels (integral-image rings for octaves 0/1,
@@ -174,6 +174,21 @@ def test_rotated_descriptor_kernels(surf, orc, monkeypatch, extend, atomic):
         again = gpu_run(surf, param, frames, w, h)
         for f in range(2):
             assert again["desc"][f].tobytes() == res["desc"][f].tobytes()
+
+
+@pytest.mark.parametrize("upright", [True, False])
+def test_single_frame_gather_plan(surf, orc, monkeypatch, upright):
+    """Config #2 as a single-frame detector (max_batch 1) on its default plan:
+    every octave on the gather Hessian kernel; keypoints/descriptors as the oracle."""
+    monkeypatch.delenv("SURFHIP_HESS_GATHER", raising=False)
+    w, h = 1920, 1080
+    frames = surf.synth_frames(1, w, h, first=7)
+    param = surf.make_param(4, 4.0, upright=upright)
+    res = gpu_run(surf, param, frames, w, h)
+    op = orc.make_param(4, 4.0, upright=upright)
+    o_pts, o_desc, nc = orc.detect(op, frames[0], w, h)
+    assert res["cand"][0] == nc
+    compare_frame(res["pts"][0], res["desc"][0], o_pts, o_desc, upright)
 
 
 @pytest.mark.parametrize("index", [0, 56])
