@@ -94,8 +94,10 @@ struct FarPlan {
 };
 // max_batch <= kGatherBatch (or SURFHIP_HESS_GATHER=1; =0 disables) puts every
 // octave on the one-thread-per-response gather kernel: the streaming kernels
-// walk whole strips, one wave each, too few waves to fill the chip for 1-2 frames.
-constexpr int kGatherBatch = 2;
+// walk whole strips, one wave each, too few waves to fill the chip for a few
+// frames (measured crossover, 1080p: gather 9,956 vs streaming 7,981 frames/s
+// at 8 frames, 12,474 vs 14,085 at 16).
+constexpr int kGatherBatch = 8;
 void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, FarPlan& far, int max_batch);
 
 // frames may be null (no u8 source known): every octave then reads the integral image

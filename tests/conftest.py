@@ -18,7 +18,7 @@ import pytest
 
 
 # The parity tests run small batches; keep them on the streaming Hessian
-# kernels the batched path uses (a detector with max_batch <= 2 would pick the
+# kernels the batched path uses (a detector with max_batch <= 8 would pick the
 # gather kernel); tests of the gather plan set SURFHIP_HESS_GATHER=1 themselves.
 os.environ.setdefault("SURFHIP_HESS_GATHER", "0")
 
