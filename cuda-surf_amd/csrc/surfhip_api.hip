@@ -300,6 +300,7 @@ static int derive(surfhip_detector* d)
     P.mag = p.mag_factor;
     P.osz = p.orient_size;
     P.nfeat = p.nfeatures;
+    P.doubled = p.doubled ? 1 : 0;
 
     int sw[kMaxOct], sh[kMaxOct], sp[kMaxOct];
     long long off = 0;

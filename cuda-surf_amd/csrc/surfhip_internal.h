@@ -46,6 +46,7 @@ struct FrameParams {
     int max_scale, init_lobe, sampling, noct;
     float thresh, divisor;
     int upright, extend, wsz, mag, osz, nfeat;
+    int doubled;                    // the integral is of the 2x frame: describe at (2x, 2y)
 };
 
 struct Tables {

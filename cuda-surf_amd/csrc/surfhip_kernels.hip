@@ -43,6 +43,24 @@ hipError_t set_tables(const Tables& t)
 __device__ __forceinline__ int f2i_rn(float v) { return (int)__builtin_rintf(v); }
 __device__ __forceinline__ int f2i_rz(float v) { return (int)v; }
 
+// Where a keypoint is described: a doubled detector's integral image is of
+// the 2x frame, so the reference samples it at (2x, 2y) with 3.3 * scale
+// for the descriptor (surfd.cu:1581-1592, 2406-2417) and 2 * scale for the
+// orientation (surfd.cu:1734-1745); otherwise (x, y) and 1.65 * scale.
+struct DescAt {
+    float x, y, scale;
+};
+template <typename PT>
+__device__ __forceinline__ DescAt desc_at(int doubled, const PT& p)
+{
+    return doubled ? DescAt{p.x + p.x, p.y + p.y, 3.3f * p.scale} : DescAt{p.x, p.y, 1.65f * p.scale};
+}
+template <typename PT>
+__device__ __forceinline__ DescAt ori_at(int doubled, const PT& p)
+{
+    return doubled ? DescAt{p.x + p.x, p.y + p.y, p.scale + p.scale} : DescAt{p.x, p.y, p.scale};
+}
+
 __device__ __forceinline__ unsigned lane_id()
 {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -591,6 +609,8 @@ __global__ __launch_bounds__(o0::THREADS, 4) void k_hess_o0(const int32_t* __res
 #include "surfhip_hess_v0.inc"
 #include "surfhip_hess_v1.inc"
 #include "surfhip_hess_vfar.inc"
+#include "surfhip_hess_s0.inc"
+#include "surfhip_hess_f0.inc"
 
 // ----------------------------------------------------------------------
 // Octave 1 (4 px between samples, lobes 15/19/23: corner offsets -34..35):
@@ -1183,6 +1203,29 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
                                                             plan.o0_vstrips, nframes);
             k_hess_v0<4, 1, 0x10><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
                                                             plan.o0_vstrips, nframes);
+        } else if (split == 20) {   // one wave per scale
+            const int ns = plan.o0_vstrips;
+            const int nb = (nframes >= 8 ? nf8 : nframes) * ns;
+            k_hess_s0<<<dim3(nb), s0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0], ns, nframes);
+        } else if (split == 21) {   // packed fp32, segment pairs
+            const int ns = plan.o0_vstrips;
+            const OctaveParams& q = h_oct[0];
+            const int npairs = (q.sh + 2 * f0::MAXSEG - 1) / (2 * f0::MAXSEG);
+            const int segr = (q.sh + 2 * npairs - 1) / (2 * npairs);
+            const int nb = (nframes >= 8 ? nf8 : nframes) * ns * npairs;
+            k_hess_f0<<<dim3(nb), f0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, q, ns, npairs, segr, nframes);
+        } else if (split == 10) {   // experiments
+            k_hess_v0<4, 0, 0x1f><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
+                                                            plan.o0_vstrips, nframes);
+        } else if (split == 11) {
+            k_hess_v0<4, 1, 0x1f, 1><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
+                                                               plan.o0_vstrips, nframes);
+        } else if (split == 12) {
+            k_hess_v0<4, 1, 0x1f, 2><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
+                                                               plan.o0_vstrips, nframes);
+        } else if (split == 13) {
+            k_hess_v0<4, 0, 0x1f, 2><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
+                                                               plan.o0_vstrips, nframes);
         } else {
             k_hess_v0<4, 1, 0x1f><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
                                                             plan.o0_vstrips, nframes);
@@ -1903,10 +1946,11 @@ __device__ float orientation_wave(const uint32_t* __restrict__ I, const FramePar
                                   OriScratch& S, unsigned lane)
 {
     const int ip = P.ip;
-    const float scale = p.scale;
+    const DescAt at = ori_at(P.doubled, p);
+    const float scale = at.scale;
     const int pixsi = f2i_rz(2.f * scale + 1.6f);
     const int pixsi2 = f2i_rz(scale + 0.8f);
-    const int ixo = f2i_rn(p.x), iyo = f2i_rn(p.y);
+    const int ixo = f2i_rn(at.x), iyo = f2i_rn(at.y);
     for (int t = lane; t < 6 * 72; t += 64) (&S.bmask[0][0])[t] = 0ull;
     wave_sync();
     for (int t = lane; t < 361; t += 64) {
@@ -2062,14 +2106,15 @@ __global__ __launch_bounds__(256) void k_describe(const int32_t* __restrict__ ii
         }
         for (int t = lane; t < 4 * DSTR; t += 64) d0[t] = 0.f;
         wave_sync();
-        const float scale = 1.65f * p.scale;
+        const DescAt at = desc_at(P.doubled, p);
+        const float scale = at.scale;
         const int step = max(f2i_rn(scale * 0.5f), 1);
-        const int ix = f2i_rn(p.x), iy = f2i_rn(p.y);
+        const int ix = f2i_rn(at.x), iy = f2i_rn(at.y);
         const float spacing = scale * (float)P.mag;
         const int hs = f2i_rz(scale);
         const int rlim = P.iH - 1 - hs, clim = P.W - hs;   // whps[1].y-1-s, whps[1].x-1-s
         if constexpr (UPRIGHT) {
-            const float dx0 = p.x - (float)ix, dy0 = p.y - (float)iy;
+            const float dx0 = at.x - (float)ix, dy0 = at.y - (float)iy;
             const int iradius = f2i_rn(((spacing * (float)(wsz + 1)) * 0.5f) / (float)step);
             const int side = 2 * iradius + 1;
             const int nsamp = side * side;
@@ -2092,7 +2137,7 @@ __global__ __launch_bounds__(256) void k_describe(const int32_t* __restrict__ ii
                 }
             }
         } else {
-            const float fracx = p.x - (float)ix, fracy = p.y - (float)iy;
+            const float fracx = at.x - (float)ix, fracy = at.y - (float)iy;
             const float sine = sincos_poly(ori, 0), cose = sincos_poly(ori, 1);
             const float fracc = ((-sine) * fracy) + (cose * fracx);
             const float fracr = (cose * fracy) + (sine * fracx);
@@ -2193,13 +2238,14 @@ __global__ __launch_bounds__(256) void k_describe_rot(const int32_t* __restrict_
         const float ori = orientation_wave(I, P, p, S.ori, lane);
         if (lane == 0) pp->ori = ori;
 
-        const float scale = 1.65f * p.scale;
+        const DescAt at = desc_at(P.doubled, p);
+        const float scale = at.scale;
         const int step = max(f2i_rn(scale * 0.5f), 1);
-        const int ix = f2i_rn(p.x), iy = f2i_rn(p.y);
+        const int ix = f2i_rn(at.x), iy = f2i_rn(at.y);
         const float spacing = scale * (float)P.mag;
         const int hs = f2i_rz(scale);
         const int rlim = P.iH - 1 - hs, clim = P.W - hs;
-        const float fracx = p.x - (float)ix, fracy = p.y - (float)iy;
+        const float fracx = at.x - (float)ix, fracy = at.y - (float)iy;
         const float sine = sincos_poly(ori, 0), cose = sincos_poly(ori, 1);
         const float fracc = ((-sine) * fracy) + (cose * fracx);
         const float fracr = (cose * fracy) + (sine * fracx);
@@ -2452,10 +2498,11 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
         }
         const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
         const __amdgpu_buffer_rsrc_t rsrc = frame_rsrc(I, P.ii_stride * 4);
-        const float scale = 1.65f * p.scale;
+        const DescAt at = desc_at(P.doubled, p);
+        const float scale = at.scale;
         const int step = max(f2i_rn(scale * 0.5f), 1);
-        const int ix = f2i_rn(p.x), iy = f2i_rn(p.y);
-        const float dx0 = p.x - (float)ix, dy0 = p.y - (float)iy;
+        const int ix = f2i_rn(at.x), iy = f2i_rn(at.y);
+        const float dx0 = at.x - (float)ix, dy0 = at.y - (float)iy;
         const float spacing = scale * (float)P.mag;
         const int hs = f2i_rz(scale);
         const int rlim = P.iH - 1 - hs, clim = P.W - hs;

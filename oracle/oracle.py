@@ -82,6 +82,9 @@ _L.or_test_box.argtypes = [_vp, _i, _i, _i, _i, _i]
 _L.or_test_place.argtypes = [_vp, _i, _i, C.c_float, _i, C.c_float, _i, C.c_float, C.c_float]
 
 _L.or_double_image.argtypes = [_vp, _i, _i, _i, _vp, _i]
+_L.or_orientation.restype = C.c_float
+_L.or_orientation.argtypes = [C.POINTER(Param), C.POINTER(Geom), _vp, _vp, _vp, _vp]
+_L.or_describe.argtypes = [C.POINTER(Param), C.POINTER(Geom), _vp, _vp, _vp, _vp]
 _L.or_match.argtypes = [_vp, _vp, _vp, _vp, _i, _i, _i, _i]
 
 lib = _L
@@ -128,6 +131,25 @@ def double_image(img: np.ndarray, w: int, h: int) -> np.ndarray:
     out = np.zeros((2 * h - 2, 2 * w - 2), np.uint8)
     _L.or_double_image(img.ctypes.data, w, h, img.shape[1], out.ctypes.data, out.shape[1])
     return out
+
+
+def describe_points(p: Param, g: Geom, ii: np.ndarray, pts: np.ndarray, orient: bool = True):
+    """or_orientation (rotated) + or_describe of given points on an integral
+    image: (ori[n], desc[n, nf]); the points' own ori is used when
+    orient is False."""
+    l1, l2, bins = tables()
+    ii = np.ascontiguousarray(ii, np.int32)
+    pts = np.ascontiguousarray(pts, dtype=POINT_DTYPE).copy()
+    desc = np.zeros((len(pts), p.nfeatures), np.float32)
+    for i in range(len(pts)):
+        pp = pts[i:i + 1]
+        if not p.upright and orient:
+            pts["ori"][i] = _L.or_orientation(C.byref(p), C.byref(g), ii.ctypes.data, l1.ctypes.data,
+                                              bins.ctypes.data, pp.ctypes.data)
+            pp = pts[i:i + 1]
+        _L.or_describe(C.byref(p), C.byref(g), ii.ctypes.data, l2.ctypes.data, pp.ctypes.data,
+                       desc[i].ctypes.data)
+    return pts["ori"].copy(), desc
 
 
 def hessian(p: Param, img: np.ndarray, w: int, h: int):

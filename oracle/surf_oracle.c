@@ -622,8 +622,11 @@ float or_cosf(float x) { return sincos_poly(x, 1); }
 float or_orientation(const or_param* p, const or_geom* g, const int32_t* ii,
                      const float lut1[83], const float bins[OR_NBIN], const or_point* pt)
 {
-    (void)p;
-    const float scale = pt->scale, x = pt->x, y = pt->y;
+    /* a doubled detector's integral is of the 2x frame: sample it at
+     * (2x, 2y) with 2 * scale (surfd.cu:1734-1745) */
+    const float scale = p->doubled ? pt->scale + pt->scale : pt->scale;
+    const float x = p->doubled ? pt->x + pt->x : pt->x;
+    const float y = p->doubled ? pt->y + pt->y : pt->y;
     const int pixsi = f2i_rz(2.f * scale + 1.6f);
     const int pixsi2 = f2i_rz(scale + 0.8f);
     const int ixo = f2i_rn(x), iyo = f2i_rn(y);
@@ -768,8 +771,11 @@ void or_describe(const or_param* p, const or_geom* g, const int32_t* ii,
     const int nf = p->nfeatures, wsz = p->desc_wsz, osz = p->orient_size;
     const int ip = g->iwhp.z;
     memset(desc, 0, sizeof(float) * nf);
-    const float x = pt->x, y = pt->y;
-    const float scale = 1.65f * pt->scale;
+    /* doubled: (2x, 2y) and 3.3 * scale in the doubled integral image
+     * (surfd.cu:1581-1592 upright, 2406-2417 rotated) */
+    const float x = p->doubled ? pt->x + pt->x : pt->x;
+    const float y = p->doubled ? pt->y + pt->y : pt->y;
+    const float scale = p->doubled ? 3.3f * pt->scale : 1.65f * pt->scale;
     const int step = f2i_rn(scale * 0.5f) > 1 ? f2i_rn(scale * 0.5f) : 1;
     const int ix = f2i_rn(x), iy = f2i_rn(y);
     const float spacing = scale * (float)p->mag_factor;

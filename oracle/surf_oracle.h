@@ -105,7 +105,7 @@ typedef struct {
 } or_octave;
 
 /* Surfor::init (surf.cpp:60-91).  Returns 0, or -1 for unsupported options
- * (doubled=true is out of scope). */
+ * (max_scale != 5: the NMS levels assume 5 scales per octave). */
 int  or_init_param(or_param* p, int noctaves, float thresh, bool doubled,
                    int init_mask_size, int sampling_step, bool upright,
                    bool extend, int desc_wsz);

@@ -121,7 +121,7 @@ def test_hessian_planes_bit_exact(surf, orc, w, h, noct):
 
 
 @pytest.mark.parametrize("env", ["SURFHIP_O0_RING", "SURFHIP_O1_RING", "SURFHIP_FAR_V", "SURFHIP_V0_SPLIT=1",
-                                 "SURFHIP_V0_SPLIT=2", "SURFHIP_HESS_GATHER=1"])
+                                 "SURFHIP_V0_SPLIT=2", "SURFHIP_V0_SPLIT=20", "SURFHIP_V0_SPLIT=21", "SURFHIP_HESS_GATHER=1"])
 @pytest.mark.parametrize("w,h,noct", [(640, 480, 4), (1920, 1080, 4)])
 def test_hessian_alternate_kernels_bit_exact(surf, orc, monkeypatch, env, w, h, noct):
     """The selectable Hessian kernels (integral-image rings for octaves 0/1,

@@ -457,3 +457,33 @@ def test_doubled_detect_geometry(orc):
     pts, d, nc = orc.detect(p, img, 640, 480)
     assert len(pts) > 500 and nc == len(pts)
     assert pts["x"].max() < 640 and pts["y"].max() < 480       # coordinates in source pixels
+
+
+@pytest.mark.parametrize("upright,extend", [(True, False), (False, False), (True, True), (False, True)])
+def test_doubled_describes_at_twice_the_position(orc, upright, extend):
+    """A doubled detector describes a point (x, y, scale) -- source-pixel
+    coordinates, makePoint's divisor 0.5 -- in the integral of the 2x frame D
+    at (2x, 2y) with 3.3 * scale, and orients it with 2 * scale
+    (surfd.cu:1581-1592, 1734-1745, 2406-2417).  Since 3.3f == 2 * 1.65f
+    exactly, that is bit for bit the ordinary (not doubled) description of
+    the point (2x, 2y, 2 * scale) on D itself; describing (x, y, scale) on D
+    (what round 1 did) gives different descriptors."""
+    img = np.load(os.path.join(GOLDEN, "images.npz"))["left_640x480"][100:260, 120:360]
+    h, w = img.shape
+    pd = orc.make_param(4, 4.0, doubled=True, upright=upright, extend=extend)
+    pts, desc, _ = orc.detect(pd, img, w, h)
+    assert len(pts) > 20
+    D = orc.double_image(img, w, h)
+    pn = orc.make_param(4, 4.0, doubled=False, upright=upright, extend=extend)
+    g, _ = orc.geometry(pn, 2 * w - 2, 2 * h - 2)
+    ii = orc.integral(D, 2 * w - 2, 2 * h - 2)
+    q = pts.copy()
+    q["x"] = pts["x"] * np.float32(2)
+    q["y"] = pts["y"] * np.float32(2)
+    q["scale"] = pts["scale"] * np.float32(2)
+    ori, d2 = orc.describe_points(pn, g, ii, q)
+    if not upright:
+        np.testing.assert_array_equal(ori.view(np.uint32), pts["ori"].view(np.uint32))
+    np.testing.assert_array_equal(d2.view(np.uint32), desc.view(np.uint32))
+    _, d_old = orc.describe_points(pn, g, ii, pts, orient=upright)
+    assert np.abs(d_old - desc).max() > 0.05
