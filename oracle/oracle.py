@@ -49,7 +49,8 @@ class Octave(C.Structure):
 
 def ensure_built() -> None:
     src = os.path.join(HERE, "surf_oracle.c")
-    if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+    newest = max(os.path.getmtime(src), os.path.getmtime(os.path.join(HERE, "surf_oracle.h")))
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
         subprocess.check_call(["make", "-s", "-C", HERE])
 
 
@@ -77,6 +78,8 @@ _L.or_bench_frames.restype = C.c_double
 _L.or_bench_frames.argtypes = [C.POINTER(Param), _vp, _i, _i, _i, _i, C.c_size_t, _i, _i,
                                C.POINTER(C.c_longlong)]
 _L.or_test_solve3.argtypes = [_vp, _vp]
+_L.or_test_fit.restype = C.c_float
+_L.or_test_fit.argtypes = [_vp, _vp, _i, _i, _i, _i, _i]
 _L.or_test_box.restype = C.c_uint32
 _L.or_test_box.argtypes = [_vp, _i, _i, _i, _i, _i]
 _L.or_test_place.argtypes = [_vp, _i, _i, C.c_float, _i, C.c_float, _i, C.c_float, C.c_float]
@@ -199,3 +202,19 @@ def match(pts1: np.ndarray, pts2: np.ndarray, f1: np.ndarray, f2: np.ndarray,
     _L.or_match(out.ctypes.data, pts2.ctypes.data, f1.ctypes.data, f2.ctypes.data,
                 n1, n2, nf, int(bool(full_tail)))
     return out
+
+
+REF_LIB = os.path.join(HERE, "_ref", "libref_host.so")
+
+
+def ref_host():
+    """The reference's own host C++ (oracle/ref_extract.py), or None where
+    /root/reference was not there to build it from."""
+    if not os.path.exists(REF_LIB):
+        return None
+    L = C.CDLL(REF_LIB)
+    L.ref_solve.argtypes = [_vp, _vp]
+    L.ref_fit.restype = C.c_float
+    L.ref_fit.argtypes = [_vp, _vp, _i, _i, _i, _i, _i]
+    L.ref_hessian_params.argtypes = [_i, _i, _i, _i, C.POINTER(_i), _i, _vp, _i, _i, _vp, _vp]
+    return L

@@ -949,6 +949,10 @@ void or_test_solve3(float sol[3], float sq[9])
     solve3(sol, m);
     for (int i = 0; i < 9; i++) sq[i] = m[i / 3][i % 3];
 }
+float or_test_fit(const float* src, float off[3], int s, int r, int c, int osize, int sp)
+{
+    return fit_quadratic(src, off, s, r, c, osize, sp);
+}
 uint32_t or_test_box(const int32_t* ii, int ipitch, int x1, int y1, int x2, int y2)
 {
     return box(ii, x1, y1, x2, y2, ipitch);

@@ -171,6 +171,7 @@ double or_bench_frames(const or_param* p, const uint8_t* frames, int nframes,
 
 /* Known-answer-test hooks on internal steps. */
 void     or_test_solve3(float sol[3], float sq[9]);   /* solveLinearSystem */
+float    or_test_fit(const float* src, float off[3], int s, int r, int c, int osize, int sp); /* fitQuadrat */
 uint32_t or_test_box(const int32_t* ii, int ipitch, int x1, int y1, int x2, int y2); /* getSum */
 void     or_test_place(float* desc, int wsz, int osz, float mag1, int ori1, float mag2, int ori2,
                        float rx, float cx);             /* placeInIndex */

@@ -3,7 +3,9 @@ and an independent numpy restatement, geometry against the values SURVEY.md
 derives from the reference's host code, and the frozen golden vectors."""
 from __future__ import annotations
 
+import ctypes as C
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -487,3 +489,141 @@ def test_doubled_describes_at_twice_the_position(orc, upright, extend):
     np.testing.assert_array_equal(d2.view(np.uint32), desc.view(np.uint32))
     _, d_old = orc.describe_points(pn, g, ii, pts, orient=upright)
     assert np.abs(d_old - desc).max() > 0.05
+
+
+# ---------------------------------------------------------------- pinning
+# oracle/_ref/libref_host.so is built by oracle/ref_extract.py from the
+# reference's own host C++ (surfd.cu:3082-3186 hSolveLinearSystem and
+# hFitQuadrat, surfd.cu:2833-2866 the Hessian parameter recurrence), compiled
+# as it stands with g++ -ffp-contract=off.  These tests pin the oracle's
+# restatements to it bit for bit.
+
+def _ref_or_skip(orc):
+    L = orc.ref_host()
+    if L is None:
+        if os.path.exists("/root/reference/surfd.cu"):
+            import subprocess
+            subprocess.check_call([sys.executable, os.path.join(os.path.dirname(orc.__file__), "ref_extract.py")])
+            L = orc.ref_host()
+        if L is None:
+            pytest.skip("reference sources absent: oracle/_ref not built")
+    return L
+
+
+def _solve_cases(n, rng):
+    """Random, integer, near-singular, singular, tiny/huge and NaN/inf systems."""
+    out = []
+    for k in range(n):
+        kind = k % 8
+        if kind == 0:
+            m = rng.standard_normal(9)
+        elif kind == 1:
+            m = rng.integers(-4, 5, 9).astype(np.float64)
+        elif kind == 2:
+            m = rng.standard_normal(9)
+            m[3:6] = m[0:3] * np.float32(1 + 1e-6)          # nearly dependent rows
+        elif kind == 3:
+            m = rng.standard_normal(9)
+            m[rng.integers(0, 3) * 3 + np.arange(3)] = 0     # a zero row
+        elif kind == 4:
+            m = rng.standard_normal(9) * 10.0 ** rng.integers(-30, 30, 9)
+        elif kind == 5:
+            m = rng.standard_normal(9)
+            m[[0, 4, 8]] = 0                                  # zero diagonal: forces pivoting
+        elif kind == 6:
+            m = np.zeros(9)                                   # all zero: 0/0
+        else:
+            m = rng.standard_normal(9)
+            m[rng.integers(0, 9)] = [np.nan, np.inf, -np.inf][k % 3]
+        sol = rng.standard_normal(3) * 10.0 ** rng.integers(-3, 4)
+        out.append((m.astype(np.float32), sol.astype(np.float32)))
+    return out
+
+
+def test_oracle_solver_pinned_to_reference_host_code(orc):
+    L = _ref_or_skip(orc)
+    rng = np.random.default_rng(2024)
+    cases = _solve_cases(100_000, rng)
+    bad = 0
+    for m, sol in cases:
+        m1, s1 = m.copy(), sol.copy()
+        m2, s2 = m.copy(), sol.copy()
+        orc.lib.or_test_solve3(s1.ctypes.data, m1.ctypes.data)
+        L.ref_solve(s2.ctypes.data, m2.ctypes.data)
+        if s1.tobytes() != s2.tobytes() or m1.tobytes() != m2.tobytes():
+            bad += 1
+    assert bad == 0, f"{bad} of {len(cases)} systems differ from hSolveLinearSystem"
+
+
+def test_oracle_fit_pinned_to_reference_host_code(orc):
+    L = _ref_or_skip(orc)
+    rng = np.random.default_rng(7)
+    sh, sp = 9, 16
+    osize = sh * sp
+    n = 0
+    for trial in range(4000):
+        kind = trial % 4
+        planes = rng.standard_normal((3, sh, sp)).astype(np.float32)
+        if kind == 1:
+            planes *= np.float32(1e4)
+        elif kind == 2:                                  # a flat, quantised response field
+            planes = np.round(planes * 4).astype(np.float32) / np.float32(4)
+        elif kind == 3:
+            planes[1, 4, 4] += np.float32(50)            # a clear peak
+        src = np.ascontiguousarray(planes.reshape(-1))
+        for r, c in ((4, 4), (1, 1), (7, 14), (3, 8)):
+            o1 = np.zeros(3, np.float32)
+            o2 = np.zeros(3, np.float32)
+            v1 = orc.lib.or_test_fit(src.ctypes.data, o1.ctypes.data, 1, r, c, osize, sp)
+            v2 = L.ref_fit(src.ctypes.data, o2.ctypes.data, 1, r, c, osize, sp)
+            assert np.float32(v1).tobytes() == np.float32(v2).tobytes() or (np.isnan(v1) and np.isnan(v2))
+            assert o1.tobytes() == o2.tobytes() or (np.isnan(o1).any() and np.isnan(o2).any())
+            n += 1
+    assert n == 16000
+
+
+@pytest.mark.parametrize("noct,sampling,init_mask,doubled", [(4, 2, 9, False), (5, 2, 9, False), (6, 2, 9, False),
+                                                              (4, 2, 9, True), (4, 3, 9, False), (4, 1, 9, False)])
+def test_oracle_octave_params_pinned_to_reference_host_code(orc, noct, sampling, init_mask, doubled):
+    """or_octave_params against surfd.cu:2833-2866 driven the way
+    Surfor::detectAndCompute drives it (surf.cpp:240-292: init mask
+    init_lobe - 2, border1 per octave, octave doubling)."""
+    L = _ref_or_skip(orc)
+    p = orc.make_param(noct, 4.0, doubled, init_mask, sampling, True, False, 4)
+    g, octs = orc.geometry(p, 1920, 1080)
+    ms, mo = 8, 8
+    mask_size = C.c_int(p.init_lobe - 2)                 # surf.cpp:240
+    octave = 1
+    borders = np.zeros(ms, np.int32)
+    for o in range(noct):
+        if o > 0:                                        # surf.cpp:261-264
+            border1 = ((3 * (mask_size.value + 4 * octave)) // 2) // (p.sampling * octave) + 1
+            borders[0] = borders[1] = border1
+            init_scale = 2
+        else:                                            # surf.cpp:269
+            border1 = ((3 * (mask_size.value + 6 * octave)) // 2) // (p.sampling * octave) + 1
+            init_scale = 0
+        params = np.zeros(7 * ms, np.int32)
+        norms = np.zeros(ms, np.float32)
+        L.ref_hessian_params(g.swhp[o].x, g.swhp[o].y, init_scale, p.max_scale, C.byref(mask_size), border1,
+                             borders.ctypes.data, octave, p.sampling, params.ctypes.data, norms.ctypes.data)
+        q = octs[o]
+        nsc = p.max_scale - init_scale
+        assert q.init_scale == init_scale and q.nscale == nsc
+        for i in range(nsc):
+            assert q.mask[i] == params[i], (o, i)
+            assert q.border1[i] == params[ms + i], (o, i)
+            assert q.delta == params[3 * ms + i]
+            assert (q.x2[i], q.x3[i], q.x4[i]) == (params[4 * ms + i], params[5 * ms + i], params[6 * ms + i])
+            assert np.float32(q.norm[i]).tobytes() == norms[i].tobytes()
+        assert list(q.borders)[:p.max_scale] == borders[:p.max_scale].tolist(), o
+        assert mask_size.value == q.mask[nsc - 1]
+        octave += octave
+
+
+def test_oracle_sanitizer_build():
+    """ASan + UBSan build of the oracle over every mode."""
+    import subprocess
+    here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")
+    out = subprocess.run(["make", "-s", "-C", here, "asan"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and "asan ok" in out.stdout, out.stdout[-2000:] + out.stderr[-2000:]
