@@ -104,6 +104,8 @@ _sigs = {
     "surfhip_detect_batch": (_i, [_vp, _vp, _i, _i, _sz, _vp, _vp, _vp]),
     "surfhip_detect": (_i, [_vp, _vp, _i, _vp, _i, C.POINTER(_i), C.POINTER(_vp), _i]),
     "surfhip_detector_candidates": (_i, [_vp, C.POINTER(_i), _i]),
+    "surfhip_detector_status": (_i, [_vp, C.POINTER(_i)]),
+    "surfhip_detector_capacity": (_i, [_vp, C.POINTER(_i)]),
     "surfhip_detector_set_profiling": (_i, [_vp, _i]),
     "surfhip_detector_stage_times": (_i, [_vp, C.POINTER(C.c_float)]),
     "surfhip_detector_workspace": (_i, [_vp, C.POINTER(_vp), C.POINTER(_sz), C.POINTER(_vp), C.POINTER(_sz)]),
@@ -286,6 +288,17 @@ class Detector:
         if rc not in (0, -3):
             check(rc, "candidates")
         return out
+
+    def truncated(self) -> bool:
+        """Whether the last batch dropped candidates at the candidate capacity."""
+        t = C.c_int()
+        check(_lib.surfhip_detector_status(self.h, C.byref(t)), "status")
+        return bool(t.value)
+
+    def capacity(self) -> int:
+        c = C.c_int()
+        check(_lib.surfhip_detector_capacity(self.h, C.byref(c)), "capacity")
+        return c.value
 
     def workspace(self):
         ii, iis, rs, rss = C.c_void_p(), C.c_size_t(), C.c_void_p(), C.c_size_t()

@@ -570,6 +570,7 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
     hipStream_t s = d->stream;
     const bool prof = d->profiling;
     HIPCHK(hipMemsetAsync(d->cand_count, 0, sizeof(int) * nframes, s));
+    HIPCHK(hipMemsetAsync(d->status, 0, sizeof(int), s));       // per-batch truncation flag
     HIPCHK(hipMemsetAsync(d->item_count, 0, sizeof(int) * (size_t)nframes * d->nitems, s));
     if (prof) {
         // serial, so that the stage events bracket each stage alone
@@ -598,8 +599,8 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
     HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->scan_key, d->scan_src, d->item_count,
                       d->item_off, d->cand, d->keys, d->cand_count, d->cap, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[3], s));
-    HIPCHK(launch_sort(d->cand, d->keys, d->gscratch, d->cand_count, d->cap, nframes, points, d->max_pts,
-                       counts, d->offsets, d->order, d->status, s));
+    HIPCHK(launch_sort(d->cand, d->keys, d->gscratch, d->cand_count, d->item_off, d->plan.nms_start[kMaxOct] * 4,
+                       d->cap, nframes, points, d->max_pts, counts, d->offsets, d->order, d->status, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[4], s));
     if (desc)
         HIPCHK(launch_describe(d->ii, d->P, points, d->max_pts, counts, d->offsets, d->order, nframes, desc, s));
@@ -617,14 +618,13 @@ int surfhip_detect(surfhip_detector* d, const uint8_t* image, int pitch, surfhip
     if (!d || !points || !num_pts || max_pts < 0) return SURFHIP_ERR_INVALID;
     int rc = surfhip_detect_batch(d, image, 1, pitch, 0, d->pts1, desc ? d->desc1 : nullptr, d->count1);
     if (rc) return rc;
-    int cnt = 0, st = 0;
+    // A frame with more candidates than the detector's capacity keeps the
+    // first `cap` NMS survivors in scan order (deterministic) and returns
+    // them like any other frame, as the reference returns max_pts points
+    // (surf.cpp:302-303); surfhip_detector_status() tells the caller.
+    int cnt = 0;
     HIPCHK(hipMemcpyAsync(&cnt, d->count1, sizeof(int), hipMemcpyDeviceToHost, d->stream));
-    HIPCHK(hipMemcpyAsync(&st, d->status, sizeof(int), hipMemcpyDeviceToHost, d->stream));
     HIPCHK(hipStreamSynchronize(d->stream));
-    if (st != 0) {
-        HIPCHK(hipMemsetAsync(d->status, 0, sizeof(int), d->stream));
-        return SURFHIP_ERR_CAPACITY;
-    }
     const int n = std::min(cnt, max_pts);                  // surf.cpp:303
     if (n > 0)
         HIPCHK(hipMemcpyAsync(points, d->pts1, sizeof(surfhip_point) * n, hipMemcpyDeviceToDevice, d->stream));
@@ -648,6 +648,23 @@ int surfhip_detector_candidates(surfhip_detector* d, int* h_counts, int nframes)
     int st = 0;
     HIPCHK(hipMemcpy(&st, d->status, sizeof(int), hipMemcpyDeviceToHost));
     return st ? SURFHIP_ERR_CAPACITY : SURFHIP_OK;
+}
+
+int surfhip_detector_status(surfhip_detector* d, int* truncated)
+{
+    if (!d || !truncated) return SURFHIP_ERR_INVALID;
+    int st = 0;
+    HIPCHK(hipMemcpyAsync(&st, d->status, sizeof(int), hipMemcpyDeviceToHost, d->stream));
+    HIPCHK(hipStreamSynchronize(d->stream));
+    *truncated = st & 1;
+    return SURFHIP_OK;
+}
+
+int surfhip_detector_capacity(surfhip_detector* d, int* cand_cap)
+{
+    if (!d || !cand_cap) return SURFHIP_ERR_INVALID;
+    *cand_cap = d->cap;
+    return SURFHIP_OK;
 }
 
 int surfhip_detector_set_profiling(surfhip_detector* d, int on)
@@ -710,7 +727,7 @@ int surfhip_pack_slab(surfhip_detector* d, const surfhip_point* pts, const float
                       int nframes, void* slab)
 {
     if (!d || !pts || !counts || !slab || nframes < 1 || nframes > d->max_batch) return SURFHIP_ERR_INVALID;
-    HIPCHK(launch_pack(pts, desc, counts, d->offsets, nframes, d->max_pts, d->param.nfeatures, (uint8_t*)slab,
+    HIPCHK(launch_pack(pts, desc, counts, d->offsets, nframes, d->max_pts, d->param.nfeatures, d->status, (uint8_t*)slab,
                        d->stream));
     return SURFHIP_OK;
 }

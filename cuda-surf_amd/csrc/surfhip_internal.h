@@ -18,6 +18,7 @@ namespace surfhip {
 constexpr int kMaxOct = 8;
 constexpr int kMaxScale = 8;
 constexpr int kSortCap = 16384;     // candidates per frame sorted in LDS
+constexpr uint32_t kNoKey = 0xffffffffu;   // candidate slot of a rejected NMS survivor
 constexpr int kBandRows = 32;       // integral-image band height
 constexpr int kScanRows = 16;       // NMS block rows per scan workgroup (4 per wave)
 constexpr int kItemCap = 64 * (kScanRows / 4);   // 2x2x2 blocks (= survivor slots) per scan item
@@ -112,8 +113,10 @@ hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const F
                       int* item_count, int* item_off, surfhip_point* cand, uint32_t* keys, int* cand_count, int cap,
                       hipStream_t s);
 hipError_t launch_sort(const surfhip_point* cand, const uint32_t* keys, uint64_t* gscratch,
-                       int* cand_count, int cap, int nframes, surfhip_point* out, int max_pts,
-                       int* out_count, int* offsets, int* order, int* status, hipStream_t s);
+                       const int* cand_count, const int* soff, int items_per_frame, int cap, int nframes,
+                       surfhip_point* out, int max_pts, int* out_count, int* offsets, int* order, int* status,
+                       hipStream_t s);
+hipError_t set_max_lds(const void* fn, int bytes);
 hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
                            const int* counts, const int* offsets, const int* order, int nframes, float* desc,
                            hipStream_t s);
@@ -126,6 +129,6 @@ size_t match_scratch_bytes(int n1, int n2, int flags);
 hipError_t launch_match(surfhip_point* pts1, const surfhip_point* pts2, const float* f1, const float* f2, int n1,
                         int n2, int nf, int flags, void* scratch, hipStream_t s);
 hipError_t launch_pack(const surfhip_point* pts, const float* desc, const int* counts, const int* offsets,
-                       int nframes, int max_pts, int nfeat, uint8_t* slab, hipStream_t s);
+                       int nframes, int max_pts, int nfeat, const int* status, uint8_t* slab, hipStream_t s);
 
 }  // namespace surfhip

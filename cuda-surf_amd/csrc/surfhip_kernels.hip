@@ -19,7 +19,9 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
+#include <mutex>
 #include <type_traits>
 #include <utility>
 
@@ -38,6 +40,36 @@ __constant__ Tables c_tab;
 hipError_t set_tables(const Tables& t)
 {
     return hipMemcpyToSymbol(HIP_SYMBOL(c_tab), &t, sizeof(Tables), 0, hipMemcpyHostToDevice);
+}
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) is per device: remember
+// per (kernel, device) that it was set (a process may drive several GPUs,
+// from several threads)
+hipError_t set_max_lds(const void* fn, int bytes)
+{
+    constexpr int kFns = 8, kDevs = 64;
+    static const void* fns[kFns] = {};
+    static std::atomic<unsigned long long> done[kFns];
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= kDevs) return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    static std::mutex mu;
+    int slot = -1;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (int i = 0; i < kFns && slot < 0; i++)
+            if (fns[i] == fn || fns[i] == nullptr) {
+                fns[i] = fn;
+                slot = i;
+            }
+    }
+    if (slot < 0) return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    const unsigned long long bit = 1ull << dev;
+    if (done[slot].load(std::memory_order_acquire) & bit) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) done[slot].fetch_or(bit, std::memory_order_release);
+    return e;
 }
 
 __device__ __forceinline__ int f2i_rn(float v) { return (int)__builtin_rintf(v); }
@@ -920,13 +952,22 @@ __device__ __forceinline__ int octave_of(const int* start, int noct, int b)
 // (blockIdx % 8) take frames x, x + 8, ..., each frame's `per` workgroups
 // together, so a frame's integral image / response planes are fetched into
 // one XCD's L2 instead of all eight.
+// Batches of fewer than 8 frames spread each frame's workgroups over all
+// XCDs instead (one frame per XCD would leave the others idle); the grid is
+// frame_grid(nframes) * per.
 __device__ __forceinline__ bool xcd_frame_block(int per, int nframes, int& f, int& lb)
 {
+    if (nframes < 8) {
+        f = blockIdx.x / per;
+        lb = blockIdx.x - f * per;
+        return f < nframes;
+    }
     const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
     f = (k / per) * 8 + xcd;
     lb = k - (k / per) * per;
     return f < nframes;
 }
+static inline int frame_grid(int nframes) { return nframes < 8 ? nframes : (nframes + 7) & ~7; }
 
 // All octaves (not on an LDS ring) of a frame in one launch: the local block
 // index walks the octaves' sample grids (64 x 4 samples per block).
@@ -1165,13 +1206,8 @@ template <int NI, int H>
 static hipError_t launch_far(const int32_t* ii, float* resp, int nframes, const FrameParams& P,
                              const OctaveParams* d_oct, const FarPlan& far, hipStream_t s)
 {
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_hess_far<NI, H>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    hipError_t e = set_max_lds(reinterpret_cast<const void*>(&k_hess_far<NI, H>), 160 * 1024);
+    if (e != hipSuccess) return e;
     const int nf8 = (nframes + 7) & ~7;
     k_hess_far<NI, H><<<dim3(nf8 * far.nstrips), farc::THREADS, far.lds_bytes, s>>>(ii, resp, P, d_oct, far, nframes);
     return hipSuccess;
@@ -1264,7 +1300,8 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
         if (e != hipSuccess) return e;
     }
     if (plan.hess_start[kMaxOct] > 0 && iip)
-        k_hessian<<<dim3(nf8 * plan.hess_start[kMaxOct]), 256, 0, s>>>(ii, resp, P, d_oct, plan, nframes);
+        k_hessian<<<dim3(frame_grid(nframes) * plan.hess_start[kMaxOct]), 256, 0, s>>>(ii, resp, P, d_oct, plan,
+                                                                                        nframes);
     return hipGetLastError();
 }
 
@@ -1697,20 +1734,28 @@ __global__ __launch_bounds__(256) void k_nms_fit(const int32_t* __restrict__ ii,
             const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
             ok = nms_fit_point(I, V, P, q, o, (int)(src >> 28), (int)((src >> 14) & 0x3fffu), (int)(src & 0x3fffu), pt);
         }
-        // a wave spans at most a few frames: append frame by frame
+        // Survivor t of frame f goes to slot t - (f's first survivor): the
+        // slots are the survivors' scan order, so which candidates a frame
+        // with more than `cap` survivors keeps is deterministic (the first
+        // cap survivors; k_sort then orders them canonically).  A rejected
+        // survivor leaves an invalid key, sorted last.
+        if (act) {
+            const int slot = t - soff[f * items_per_frame];
+            if (slot < cap) {
+                if (ok) cand[(size_t)f * cap + slot] = pt;
+                keys[(size_t)f * cap + slot] = ok ? key : kNoKey;
+            }
+        }
+        // accepted candidates per frame (a wave spans at most a few frames);
+        // k_sort compares it with the ones inside the cap to flag truncation
         bool pending = ok;
         while (__ballot(pending)) {
             const int leader = __builtin_ctzll(__ballot(pending));
             const int ff = __shfl(f, leader, 64);
             const bool mine = pending && f == ff;
-            const int slot = wave_append(mine, &cand_count[ff]);
-            if (mine) {
-                if (slot < cap) {
-                    cand[(size_t)ff * cap + slot] = pt;
-                    keys[(size_t)ff * cap + slot] = key;
-                }
-                pending = false;
-            }
+            const unsigned long long m = __ballot(mine);
+            if ((int)lane_id() == leader) atomicAdd(&cand_count[ff], __popcll(m));
+            if (mine) pending = false;
         }
     }
 }
@@ -1722,8 +1767,8 @@ hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const F
 {
     const int per = plan.nms_start[kMaxOct];
     if (per == 0) return hipSuccess;
-    k_nms_scan<<<dim3(((nframes + 7) & ~7) * per), 256, 0, s>>>(resp, P, d_oct, plan, scan_key, scan_src, item_count,
-                                                                 nframes);
+    k_nms_scan<<<dim3(frame_grid(nframes) * per), 256, 0, s>>>(resp, P, d_oct, plan, scan_key, scan_src, item_count,
+                                                                nframes);
     const int nitems = nframes * per * 4;
     launch_excl_scan(item_count, nitems, item_off, item_off + nitems + 1, s);
     k_nms_fit<<<kFitGrid, 256, 0, s>>>(ii, resp, P, d_oct, scan_key, scan_src, item_off, nitems, per * 4, cand, keys,
@@ -1758,30 +1803,35 @@ __device__ void bitonic_sort(PtrT s, int n)
 
 __global__ __launch_bounds__(1024) void k_sort(const surfhip_point* __restrict__ cand,
                                                const uint32_t* __restrict__ keys,
-                                               uint64_t* __restrict__ gscratch, int* cand_count, int cap,
+                                               uint64_t* __restrict__ gscratch, const int* __restrict__ cand_count,
+                                               const int* __restrict__ soff, int items_per_frame, int cap,
                                                surfhip_point* __restrict__ out, int max_pts,
                                                int* __restrict__ out_count, int* __restrict__ order, int* status)
 {
     extern __shared__ __attribute__((aligned(16))) uint64_t sk[];
+    __shared__ int nvalid;
     const int f = blockIdx.x;
-    int cnt = cand_count[f];
-    if (cnt > cap) {
-        if (threadIdx.x == 0) atomicOr(status, 1);
-        cnt = cap;
-    }
+    // slots written by k_nms_fit: the frame's survivors, at most cap
+    const int cnt = min(soff[(f + 1) * items_per_frame] - soff[f * items_per_frame], cap);
     int n = 1;
-    while (n < cnt) n <<= 1;
+    while (n < cnt) n <<= 1;                  // <= cap (a power of 2)
     const bool in_lds = n <= kSortCap;
     uint64_t* s = in_lds ? sk : gscratch + (size_t)f * cap;
-    if (!in_lds && n > cap) {          // gscratch holds cap entries per frame
-        if (threadIdx.x == 0) atomicOr(status, 2);
-        return;
+    if (threadIdx.x == 0) nvalid = 0;
+    __syncthreads();
+    int mine = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t k = (i < cnt) ? keys[(size_t)f * cap + i] : kNoKey;
+        mine += k != kNoKey;
+        s[i] = ((uint64_t)k << 32) | (uint32_t)i;
     }
-    for (int i = threadIdx.x; i < n; i += blockDim.x)
-        s[i] = (i < cnt) ? (((uint64_t)keys[(size_t)f * cap + i] << 32) | (uint32_t)i) : ~0ull;
+    if (mine) atomicAdd(&nvalid, mine);
     __syncthreads();
     bitonic_sort(s, n);
-    const int keep = min(cnt, max_pts);
+    const int valid = nvalid;
+    // accepted candidates beyond the cap were dropped: report it
+    if (threadIdx.x == 0 && cand_count[f] > valid) atomicOr(status, 1);
+    const int keep = min(valid, max_pts);
     for (int t = threadIdx.x; t < keep; t += blockDim.x)
         out[(size_t)f * max_pts + t] = cand[(size_t)f * cap + (uint32_t)(s[t] & 0xffffffffu)];
     if (threadIdx.x == 0) out_count[f] = keep;
@@ -1812,19 +1862,15 @@ __global__ __launch_bounds__(1024) void k_offsets(const int* __restrict__ counts
 }
 
 hipError_t launch_sort(const surfhip_point* cand, const uint32_t* keys, uint64_t* gscratch,
-                       int* cand_count, int cap, int nframes, surfhip_point* out, int max_pts,
-                       int* out_count, int* offsets, int* order, int* status, hipStream_t s)
+                       const int* cand_count, const int* soff, int items_per_frame, int cap, int nframes,
+                       surfhip_point* out, int max_pts, int* out_count, int* offsets, int* order, int* status,
+                       hipStream_t s)
 {
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)(kSortCap * sizeof(uint64_t)));
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
-    k_sort<<<nframes, 1024, kSortCap * sizeof(uint64_t), s>>>(cand, keys, gscratch, cand_count, cap, out,
-                                                              max_pts, out_count, order, status);
+    hipError_t e = set_max_lds(reinterpret_cast<const void*>(&k_sort), (int)(kSortCap * sizeof(uint64_t)));
+    if (e != hipSuccess) return e;
+    k_sort<<<nframes, 1024, kSortCap * sizeof(uint64_t), s>>>(cand, keys, gscratch, cand_count, soff,
+                                                              items_per_frame, cap, out, max_pts, out_count, order,
+                                                              status);
     k_offsets<<<1, 1024, 0, s>>>(out_count, nframes, offsets);
     return hipGetLastError();
 }
@@ -2962,13 +3008,15 @@ hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_poin
 // ======================================================================
 __global__ __launch_bounds__(256) void k_pack(const surfhip_point* __restrict__ pts, const float* __restrict__ desc,
                                               const int* __restrict__ counts, const int* __restrict__ offsets,
-                                              int nframes, int max_pts, int nfeat, uint8_t* __restrict__ slab)
+                                              int nframes, int max_pts, int nfeat, const int* __restrict__ status,
+                                              uint8_t* __restrict__ slab)
 {
     const int f = blockIdx.y;
     const int total = offsets[nframes];
     int* hdr = reinterpret_cast<int*>(slab);
     if (f == 0 && blockIdx.x == 0) {
-        if (threadIdx.x == 0) { hdr[0] = nframes; hdr[1] = total; hdr[2] = desc ? nfeat : 0; hdr[3] = 0; }
+        // hdr[3] bit 0: a frame of this batch was truncated at the candidate capacity
+        if (threadIdx.x == 0) { hdr[0] = nframes; hdr[1] = total; hdr[2] = desc ? nfeat : 0; hdr[3] = status ? (*status & 1) : 0; }
         const int npad = (nframes + 3) & ~3;          // counts padded to 16 B with zeros (stable file bytes)
         for (int i = threadIdx.x; i < npad; i += 256) hdr[4 + i] = i < nframes ? counts[i] : 0;
     }
@@ -2988,9 +3036,9 @@ __global__ __launch_bounds__(256) void k_pack(const surfhip_point* __restrict__ 
 }
 
 hipError_t launch_pack(const surfhip_point* pts, const float* desc, const int* counts, const int* offsets,
-                       int nframes, int max_pts, int nfeat, uint8_t* slab, hipStream_t s)
+                       int nframes, int max_pts, int nfeat, const int* status, uint8_t* slab, hipStream_t s)
 {
-    k_pack<<<dim3(16, nframes), 256, 0, s>>>(pts, desc, counts, offsets, nframes, max_pts, nfeat, slab);
+    k_pack<<<dim3(16, nframes), 256, 0, s>>>(pts, desc, counts, offsets, nframes, max_pts, nfeat, status, slab);
     return hipGetLastError();
 }
 

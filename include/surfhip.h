@@ -145,8 +145,19 @@ int surfhip_detect(surfhip_detector* det, const uint8_t* d_image, int pitch,
                    float** d_desc_out, int desc);
 
 /* Raw candidate count per frame of the last call (before the max_pts clamp,
- * surf.cpp:302-303); host array of nframes ints. */
+ * surf.cpp:302-303); host array of nframes ints.  Returns
+ * SURFHIP_ERR_CAPACITY (counts still written) when the last batch truncated
+ * a frame at the candidate capacity. */
 int surfhip_detector_candidates(surfhip_detector* det, int* h_counts, int nframes);
+
+/* Did the last detect_batch / detect drop accepted candidates because a
+ * frame had more NMS survivors than the candidate capacity (cand_cap of
+ * surfhip_detector_create, rounded up to a power of 2)?  Such a frame keeps
+ * its first cand_cap survivors in scan order -- deterministic -- sorted
+ * canonically, then the first max_pts (the reference keeps an arbitrary
+ * subset, surfd.cu:822-831).  The flag is reset by every batch. */
+int surfhip_detector_status(surfhip_detector* det, int* truncated);
+int surfhip_detector_capacity(surfhip_detector* det, int* cand_cap);
 
 /* Stage timing (HIP events on the detector's stream) for the last
  * detect_batch: ms[0..5] = integral, hessian, nms, sort, describe, total. */
@@ -175,7 +186,8 @@ long long surfhip_hessian_bytes_per_frame(surfhip_detector* det);
 
 /* Result slab for the multi-GPU all-gather, compacted to the
  * keypoints actually found by the last detect_batch:
- *   int32 {nframes, total, nfeatures (0 without descriptors), 0}
+ *   int32 {nframes, total, nfeatures (0 without descriptors), flags}
+ *     (flags bit 0: a frame was truncated at the candidate capacity)
  *   int32 counts[nframes] padded to 16 B
  *   SurfPoint points[total]          (frame-major, canonical order)
  *   float desc[total][nfeatures]

@@ -841,10 +841,19 @@ void or_describe(const or_param* p, const or_geom* g, const int32_t* ii,
             }
         }
     }
-    /* normalize: sequential-addressing tree (surfd.cu:2460-2487) */
+    /* normalize (surfd.cu:2447-2493): the squares, zero-padded to
+     * P = max(64, next power of two >= nf), summed by the sequential-
+     * addressing tree (strides P/2 .. 1).  For nf = 64 / 128 -- the sizes of
+     * desc_wsz 4 -- this is the reference's order exactly (its stride loop
+     * down to 64, then the warp-synchronous 32 .. 1).  For other window
+     * sizes the reference reads its nfeatures-float shared array out of
+     * bounds (tid + 32 >= nf) or, for nf = 72, adds squares twice; here it
+     * is defined as the full sum, which the HIP kernels compute too. */
     float sq[128];
-    for (int t = 0; t < nf; t++) sq[t] = desc[t] * desc[t];
-    for (int stride = nf / 2; stride >= 1; stride >>= 1)
+    int P = 64;
+    while (P < nf) P <<= 1;
+    for (int t = 0; t < P; t++) sq[t] = t < nf ? desc[t] * desc[t] : 0.f;
+    for (int stride = P / 2; stride >= 1; stride >>= 1)
         for (int t = 0; t < stride; t++) sq[t] = sq[t] + sq[t + stride];
     const float fac = 1.f / sqrtf(sq[0]);
     for (int t = 0; t < nf; t++) desc[t] = desc[t] * fac;

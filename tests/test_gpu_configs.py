@@ -1,0 +1,167 @@
+"""GPU parity at the configurations the bench and BASELINE.json run.
+
+- config #3: one 256-frame 1920x1080 batch (the bench's workload, streaming
+  Hessian plan, XCD frame mapping) -- frames 0, 7, 8, 127, 255 against the
+  oracle, and every frame against a single-frame detector (whose default plan
+  is the gather Hessian: a second, independent path);
+- config #5: 3840x2160, 5 octaves, rotated, 128-D extended, as an 8-frame
+  batch -- keypoints and ori bit-exact, descriptors within 1e-4 L2;
+- the candidate sort beyond the LDS capacity (> 16,384 candidates, global
+  scratch path) and deterministic truncation at a small candidate capacity;
+- descriptor windows other than 4 (the generic k_describe);
+- the single-frame gather plan on the doubled, 5/6-octave and rotated cases.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import assert_points_equal, desc_l2
+from test_gpu_parity import DESC_TOL, compare_frame, gpu_run
+
+pytestmark = pytest.mark.gpu
+
+W3, H3 = 1920, 1080
+
+
+@pytest.fixture(scope="module")
+def config3(surf):
+    frames = surf.synth_frames(256, W3, H3, first=0)
+    param = surf.make_param(4, 4.0, upright=True)
+    res = gpu_run(surf, param, frames, W3, H3, max_pts=8192)
+    return frames, res
+
+
+@pytest.mark.parametrize("f", [0, 7, 8, 127, 255])
+def test_config3_batch256_vs_oracle(orc, config3, f):
+    frames, res = config3
+    op = orc.make_param(4, 4.0, upright=True)
+    o_pts, o_desc, nc = orc.detect(op, frames[f], W3, H3, max_pts=8192)
+    assert len(o_pts) > 1000
+    assert res["cand"][f] == nc
+    compare_frame(res["pts"][f], res["desc"][f], o_pts, o_desc, True)
+
+
+def test_config3_batch256_vs_single_frame(surf, monkeypatch, config3):
+    """All 256 frames of the batch against a max_batch=1 detector, whose
+    default plan puts every octave on the gather Hessian kernel."""
+    frames, res = config3
+    monkeypatch.delenv("SURFHIP_HESS_GATHER", raising=False)
+    param = surf.make_param(4, 4.0, upright=True)
+    max_pts = 8192
+    det = surf.Detector(param, W3, H3, max_batch=1, max_pts=max_pts)
+    pitch = frames.shape[2]
+    fb = surf.DeviceBuffer(frames[0].nbytes)
+    pb = surf.DeviceBuffer(48 * max_pts)
+    db = surf.DeviceBuffer(4 * max_pts * 64)
+    cb = surf.DeviceBuffer(4)
+    assert not res["truncated"]
+    for f in range(256):
+        fb.upload(frames[f])
+        det.detect_batch(fb.ptr, 1, pitch, 0, pb.ptr, db.ptr, cb.ptr)
+        surf.synchronize()
+        n = int(cb.download(np.int32, 1)[0])
+        assert n == res["counts"][f], f
+        pts = pb.download(surf.POINT_DTYPE, max_pts)[:n]
+        assert_points_equal(pts, res["pts"][f])
+        d = db.download(np.float32, max_pts * 64).reshape(max_pts, 64)[:n]
+        assert d.tobytes() == res["desc"][f].tobytes(), f
+    det.close()
+
+
+def test_config5_4k_rotated_extended(surf, orc):
+    """Config #5 layout: 3840x2160, 5 octaves, upright=false, 128-D, as an
+    8-frame batch (XCD mapping, 4K integral near the int32 limit)."""
+    w, h = 3840, 2160
+    frames = surf.synth_frames(8, w, h, first=500)
+    param = surf.make_param(5, 4.0, upright=False, extend=True)
+    res = gpu_run(surf, param, frames, w, h, max_pts=32768)
+    assert not res["truncated"]
+    op = orc.make_param(5, 4.0, upright=False, extend=True)
+    for f in (0, 7):
+        o_pts, o_desc, nc = orc.detect(op, frames[f], w, h, max_pts=32768)
+        assert len(o_pts) > 5000 and set(np.unique(o_pts["o"])) == {0, 1, 2, 3, 4}
+        assert res["cand"][f] == nc
+        compare_frame(res["pts"][f], res["desc"][f], o_pts, o_desc, False)
+
+
+def _noise(n, w, h, seed):
+    rng = np.random.default_rng(seed)
+    pitch = (w + 127) // 128 * 128
+    return rng.integers(0, 256, (n, h, pitch), dtype=np.uint8)
+
+
+def test_sort_beyond_lds_capacity(surf, orc):
+    """A noise frame at thresh 0.3 has ~21,700 keypoints: more than the
+    16,384 candidates k_sort orders in LDS, so the global-scratch bitonic sort
+    runs (candidate capacity 32,768)."""
+    frames = _noise(1, W3, H3, 1)
+    param = surf.make_param(4, 0.3, upright=False)
+    res = gpu_run(surf, param, frames, W3, H3, max_pts=32768, cand_cap=32768)
+    assert res["capacity"] == 32768 and not res["truncated"]
+    op = orc.make_param(4, 0.3, upright=False)
+    o_pts, o_desc, nc = orc.detect(op, frames[0], W3, H3, max_pts=32768)
+    assert nc > 16384
+    assert res["cand"][0] == nc
+    compare_frame(res["pts"][0], res["desc"][0], o_pts, o_desc, False)
+
+
+def test_candidate_capacity_truncation_is_deterministic(surf, orc):
+    """More NMS survivors than the candidate capacity: the frame keeps the
+    first `cap` survivors (scan order) -- the same set every run --, sorted
+    canonically, each one a keypoint of the full result, and the detector
+    reports the truncation (the reference keeps an arbitrary subset)."""
+    frames = _noise(2, W3, H3, 2)
+    param = surf.make_param(4, 0.3, upright=True)
+    a = gpu_run(surf, param, frames, W3, H3, max_pts=32768, cand_cap=4096)
+    b = gpu_run(surf, param, frames, W3, H3, max_pts=32768, cand_cap=4096)
+    full = gpu_run(surf, param, frames, W3, H3, max_pts=32768, cand_cap=32768)
+    assert a["truncated"] and b["truncated"] and not full["truncated"]
+    for f in range(2):
+        assert 0 < a["counts"][f] <= 4096
+        assert a["pts"][f].tobytes() == b["pts"][f].tobytes()
+        assert a["desc"][f].tobytes() == b["desc"][f].tobytes()
+        key = lambda p: set(zip(p["o"].tolist(), p["y"].view(np.uint32).tolist(), p["x"].view(np.uint32).tolist(),
+                                p["scale"].view(np.uint32).tolist()))
+        assert key(a["pts"][f]) <= key(full["pts"][f])
+        # canonical order: octave non-decreasing
+        assert (np.diff(a["pts"][f]["o"]) >= 0).all()
+
+
+@pytest.mark.parametrize("wsz", [2, 3])
+@pytest.mark.parametrize("upright", [True, False])
+def test_descriptor_window_sizes(surf, orc, wsz, upright):
+    """desc_wsz 2 and 3 (mag_factor 6 / 4, 16- and 36-D) on the generic
+    k_describe (surfd.cu:1566-1615, 2391-2444 with wsz != 4)."""
+    w, h = 640, 480
+    frames = surf.synth_frames(2, w, h, first=40)
+    param = surf.make_param(4, 4.0, upright=upright, desc_wsz=wsz)
+    assert param.nfeatures == wsz * wsz * 4
+    res = gpu_run(surf, param, frames, w, h)
+    op = orc.make_param(4, 4.0, upright=upright, desc_wsz=wsz)
+    for f in range(2):
+        o_pts, o_desc, _ = orc.detect(op, frames[f], w, h)
+        assert len(o_pts) > 100
+        compare_frame(res["pts"][f], res["desc"][f], o_pts, o_desc, upright)
+
+
+@pytest.mark.parametrize("case", ["doubled", "oct5", "oct6", "rotated_ext_720p"])
+def test_gather_plan_cases(surf, orc, monkeypatch, case):
+    """The single-frame plan (gather Hessian for every octave, the default
+    for max_batch <= 8) on inputs the streaming tests cover: the doubled
+    frame, 5 and 6 octaves, rotated 128-D."""
+    monkeypatch.setenv("SURFHIP_HESS_GATHER", "1")
+    doubled, noct, upright, extend, w, h = {
+        "doubled": (True, 4, True, False, 640, 480),
+        "oct5": (False, 5, True, False, 1920, 1080),
+        "oct6": (False, 6, False, False, 1920, 1080),
+        "rotated_ext_720p": (False, 5, False, True, 1280, 720),
+    }[case]
+    frames = surf.synth_frames(2, w, h, first=77)
+    param = surf.make_param(noct, 4.0, doubled=doubled, upright=upright, extend=extend)
+    res = gpu_run(surf, param, frames, w, h)
+    op = orc.make_param(noct, 4.0, doubled=doubled, upright=upright, extend=extend)
+    for f in range(2):
+        o_pts, o_desc, _ = orc.detect(op, frames[f], w, h)
+        assert len(o_pts) > 50
+        compare_frame(res["pts"][f], res["desc"][f], o_pts, o_desc, upright)

@@ -37,7 +37,7 @@ def gpu_run(surf, param, frames, w, h, max_pts=16384, desc=True, want_ws=False, 
     ds = db.download(np.float32, n * max_pts * nf).reshape(n, max_pts, nf) if desc else None
     out = {"counts": counts, "pts": [pts[f, :counts[f]] for f in range(n)],
            "desc": [ds[f, :counts[f]] for f in range(n)] if desc else None,
-           "cand": det.candidates(n)}
+           "cand": det.candidates(n), "truncated": det.truncated(), "capacity": det.capacity()}
     if want_ws:
         ii, iis, rs, rss = det.workspace()
         out["ii"] = surf.download_ptr(ii, np.int32, n * iis).reshape(n, -1)
