@@ -10,8 +10,11 @@ integral -> Hessian (all octaves) -> NMS + interpolation -> canonical sort ->
 descriptors.  With N > 1 GPUs (one process per GPU, torch.distributed over
 RCCL) each rank processes its own 256 frames (weak scaling, config #4 at
 N = 8) and the compacted SurfPoint + descriptor slab of every rank is
-all-gathered over xGMI; the gather of batch i overlaps the
-compute of batch i+1.
+all-gathered over xGMI through libsurfcomm's surfhip_allgather (SURVEY.md
+8e) into a per-rank capacity agreed once before the timed region; the gather
+of batch i overlaps the compute of batch i+1 on a comm stream.  The run fails
+(exit 3, no JSON) if any frame hit max_pts, the candidate capacity
+overflowed, or a slab exceeded its capacity.
 
 Rank 0 prints ONE JSON line (the driver's contract), with a `roofline` object
 for the Hessian kernel (HIP events on the detector's stream inside the timed
@@ -69,23 +72,27 @@ def cpu_baseline(frames, w, h, args):
 
 
 def pmc_traffic(args):
-    """Per-launch HBM bytes of the Hessian kernel from a committed rocprofv3
-    --pmc summary (profiles/*hessian_pmc.json), or None."""
+    """Per-batch HBM bytes of the Hessian stage from the committed rocprofv3
+    --pmc passes of this build (profiles/hessian_pmc.json, FETCH_SIZE +
+    WRITE_SIZE, gfx950-corrected; tools/profile_round.sh + tools/summarize_profiles.py), with the
+    profile's tag -- (bytes, tag) or (None, None).  A PMC pass cannot run
+    inside this process (rocprofv3 wraps the whole program), so the figure is
+    labelled with the run it came from."""
     path = args.pmc_json or os.path.join(REPO, "profiles", "hessian_pmc.json")
     try:
         with open(path) as fh:
             d = json.load(fh)
         if d.get("config") == f"{args.batch}x{args.width}x{args.height}x{args.octaves}":
-            return float(d["bytes_per_launch"])
+            return float(d["bytes_per_launch"]), d.get("tag")
     except (OSError, ValueError, KeyError):
         pass
-    return None
+    return None, None
 
 
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="frames per GPU per step")
     ap.add_argument("--width", type=int, default=1920)
@@ -94,7 +101,13 @@ def main():
     ap.add_argument("--upright", type=int, default=1)
     ap.add_argument("--extend", type=int, default=0)
     ap.add_argument("--thresh", type=float, default=4.0)
-    ap.add_argument("--max-pts", type=int, default=16384)
+    ap.add_argument("--max-pts", type=int, default=0,
+                    help="keypoint cap per frame (default 65,536 up to 1080p, 262,144 above; SURVEY 8d)")
+    ap.add_argument("--exchange", choices=("rccl", "gloo"), default="rccl",
+                    help="world > 1: slab all-gather through libsurfcomm (RCCL), or host-staged over gloo "
+                         "(a rehearsal that runs several ranks on one GPU)")
+    ap.add_argument("--slab-headroom", type=float, default=1.10,
+                    help="fixed per-rank slab capacity = max over ranks of the warm-up slab x this")
     ap.add_argument("--cpu-frames", type=int, default=128, help="frames per CPU baseline chunk")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline wall-time budget")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -106,6 +119,8 @@ def main():
     ap.add_argument("--with-integral", action="store_true",
                     help="with --hessian-only: run the integral before every Hessian launch")
     args = ap.parse_args()
+    if args.max_pts <= 0:
+        args.max_pts = 65536 if args.width * args.height <= 1920 * 1088 else 262144
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -114,12 +129,15 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # one process per GPU; with --exchange gloo several ranks may share a GPU
+    gpu = local % max(1, torch.cuda.device_count()) if world > 1 else 0
+    dev = torch.device("cuda", gpu)
+    torch.cuda.set_device(dev)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+        if args.exchange == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     surf = load_surf()
     surf.set_device(dev.index)
 
@@ -155,46 +173,71 @@ def main():
     if args.hessian_only:
         det.run_integral(d_frames.data_ptr(), B, pitch, H * pitch)
 
-    # multi-GPU exchange: compacted slabs, double-buffered, gather(i-1) || compute(i)
-    slabs = [None, None]
-    gathered = [None, None]
-    pending = None
+    # multi-GPU exchange: every rank packs its compacted
+    # SurfPoint + descriptor slab straight into its own section of a gather
+    # buffer of a FIXED per-rank capacity (agreed once, below) and the
+    # sections are all-gathered through the C-ABI (libsurfcomm,
+    # surfhip_allgather over RCCL) on a comm stream: no host synchronisation
+    # per step; gather(i) overlaps compute(i+1), two buffers alternate.
+    exchange = world > 1 and not args.hessian_only
+    comm = comm_stream = None
+    cap = 0
+    gathered, ev_packed, ev_gathered = [None, None], [None, None], [None, None]
+    if exchange:
+        for i in range(args.warmup):                  # the detector's steady state sizes the slab
+            run_batch()
+        used = det.slab_bytes(B, det.batch_total(B))
+        cap = surf.dist.agree_slab_size(dist, torch, used, dev)     # once, outside the timed region
+        cap = surf.align_up(int(cap * args.slab_headroom) + 64, 256)
+        for k in range(2):
+            gathered[k] = torch.empty(world * cap, dtype=torch.uint8, device=dev)
+            ev_packed[k] = torch.cuda.Event()
+            ev_gathered[k] = torch.cuda.Event()
+        comm_stream = torch.cuda.Stream(dev)
+        if args.exchange == "rccl":
+            uid = torch.zeros(surf.COMM_ID_BYTES, dtype=torch.uint8)
+            if rank == 0:
+                uid[:] = torch.frombuffer(bytearray(surf.comm_unique_id()), dtype=torch.uint8)
+            uid_d = uid.to(dev)
+            dist.broadcast(uid_d, 0)
+            comm = surf.Comm(world, rank, bytes(uid_d.cpu().numpy().tobytes()))
 
-    def launch_gather(i):
-        total = det.batch_total(B)                    # sync: sizes the collective
-        cap = surf.dist.agree_slab_size(dist, torch, det.slab_bytes(B, total), dev)
+    nstep = 0                                          # buffer i & 1 across warmup and timed steps
+
+    def gather(i):
         k = i & 1
-        if slabs[k] is None or slabs[k].numel() < cap:
-            slabs[k] = torch.empty(int(cap * 1.25) + 4096, dtype=torch.uint8, device=dev)
-            gathered[k] = torch.empty(world * slabs[k].numel(), dtype=torch.uint8, device=dev)
-        det.pack_slab(d_pts.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(), B, slabs[k].data_ptr())
-        _, work = surf.dist.allgather_slabs(dist, torch, slabs[k], cap, world, out=gathered[k], async_op=True)
-        return work
+        mine = gathered[k].data_ptr() + rank * cap
+        if i >= 2:
+            stream.wait_event(ev_gathered[k])         # gather(i-2) has read this buffer
+        det.pack_slab_cap(d_pts.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(), B, mine, cap)
+        ev_packed[k].record(stream)
+        comm_stream.wait_event(ev_packed[k])
+        if comm is not None:
+            comm.allgather(mine, cap, gathered[k].data_ptr(), comm_stream.cuda_stream)
+        else:                                         # --exchange gloo: host-staged rehearsal
+            with torch.cuda.stream(comm_stream):
+                chunks = list(gathered[k].view(world, cap).cpu().unbind(0))
+                dist.all_gather(chunks, chunks[rank].clone())
+                gathered[k].copy_(torch.cat(chunks).to(dev))
+        ev_gathered[k].record(comm_stream)
 
     def step(i):
-        nonlocal pending
+        nonlocal nstep
         run_batch()
-        if world > 1 and not args.hessian_only:
-            if pending is not None:
-                pending.wait()
-            pending = launch_gather(i)
+        if exchange:
+            gather(nstep)
+        nstep += 1
 
     for i in range(args.warmup):
         step(i)
-    if pending is not None:
-        pending.wait()
-        pending = None
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
 
-    stage_acc = {}
     t_start = time.perf_counter()
     for i in range(args.steps):
         step(i)
-    if pending is not None:
-        pending.wait()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -205,7 +248,42 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # no truncation anywhere: a frame at max_pts, a candidate-capacity
+    # overflow or a slab beyond the agreed capacity invalidates the run
     counts = d_cnt.cpu().numpy()
+    problems = []
+    if not args.hessian_only:
+        if det.truncated():
+            problems.append("candidate capacity overflow (surfhip_detector_status)")
+        if (counts >= args.max_pts).any():
+            problems.append(f"{int((counts >= args.max_pts).sum())} frames reached max_pts {args.max_pts}")
+    exchanged = None
+    if exchange:
+        last = (nstep - 1) & 1
+        g = gathered[last].cpu().numpy().reshape(world, cap)
+        totals = []
+        for r in range(world):
+            fl = surf.slab_flags(g[r])
+            if fl:
+                problems.append(f"rank {r} slab flags {fl}")
+                continue
+            c, pts, desc = surf.parse_slab(g[r])
+            if len(c) != B or (desc is not None and desc.shape[1] != nf) or len(pts) != int(c.sum()):
+                problems.append(f"rank {r} slab malformed")
+            totals.append(int(c.sum()))
+        c0, _, _ = surf.parse_slab(g[rank])
+        if not np.array_equal(c0, counts):
+            problems.append(f"rank {rank}: gathered counts differ from detect_batch's")
+        exchanged = {"backend": args.exchange, "slab_cap_bytes": cap, "gathered_bytes_per_step": world * cap,
+                     "keypoints_gathered_per_step": sum(totals)}
+    if world > 1:
+        bad = torch.tensor([len(problems)], dtype=torch.int64, device=dev)
+        dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+        if int(bad.item()) and not problems:
+            problems.append("another rank reported truncation")
+    if problems:
+        print(f"bench.py rank {rank}: INVALID RUN: " + "; ".join(problems), file=sys.stderr, flush=True)
+        sys.exit(3)
     kp_per_batch = int(counts.sum())
     if world > 1:
         kt = torch.tensor([kp_per_batch], dtype=torch.int64, device=dev)
@@ -214,6 +292,7 @@ def main():
     else:
         kp_total_batch = kp_per_batch
 
+    stage_acc = {}
     # per-stage times: a short serial pass with HIP events between the stages
     nprof = min(args.steps, 3)
     if profile and not args.hessian_only:
@@ -243,7 +322,7 @@ def main():
     if rank == 0:
         hb = det.hessian_bytes_per_frame() * B
         achieved = hb / (hess_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(args)
+        traffic, traffic_tag = pmc_traffic(args)
         if (W, H) == (1920, 1080) and args.octaves == 4:
             cfg_name = "config#3"
         elif (W, H) == (3840, 2160) and args.octaves == 5 and not args.upright and args.extend:
@@ -270,22 +349,27 @@ def main():
                        "nfeatures": nf, "upright": bool(args.upright), "parallelism": f"frames sharded x{world}"},
             "keypoints_per_s": round(kp_total_batch * args.steps / elapsed, 1),
             "keypoints_per_frame": round(kp_total_batch / (world * B), 1),
+            "keypoints_per_step": kp_total_batch,
             "stage_ms_per_step_serial": {k: round(v / nprof, 4) for k, v in stage_acc.items()},
             "roofline": {"kernel": "Hessian stage, all octaves in series: k_hess_v0 (octave 0) + k_hess_v1 "
                                    "(octave 1) + k_hess_far (octaves >= 2), per batch",
                          "bound": "hbm",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic,
+                         "traffic": traffic, "traffic_profile": traffic_tag,
                          "algorithmic_bytes_per_launch": hb, "launch_ms": round(hess_ms, 4)},
             "gen_s": round(gen_s, 2),
         }
+        if exchanged is not None:
+            result["exchange"] = exchanged
         if world == 1 and not args.no_cpu and not args.hessian_only:
             result["cpu_baseline"] = cpu_baseline(frames, W, H, args)
         else:
             result["cpu_baseline"] = None
         print(json.dumps(result), flush=True)
     det.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

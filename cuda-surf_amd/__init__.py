@@ -116,6 +116,7 @@ _sigs = {
     "surfhip_slab_bytes": (_sz, [_i, _i, _i]),
     "surfhip_batch_total": (_i, [_vp, _i, C.POINTER(_i)]),
     "surfhip_pack_slab": (_i, [_vp, _vp, _vp, _vp, _i, _vp]),
+    "surfhip_pack_slab_cap": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _sz]),
     "surfhip_match_scratch": (_sz, [_i, _i, _i]),
     "surfhip_match": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp]),
     "surfhip_ingest_create": (_i, [C.POINTER(_vp), _vp, _i]),
@@ -328,6 +329,12 @@ class Detector:
     def pack_slab(self, points_ptr, desc_ptr, counts_ptr, nframes, slab_ptr) -> None:
         check(_lib.surfhip_pack_slab(self.h, points_ptr, desc_ptr, counts_ptr, nframes, slab_ptr), "pack_slab")
 
+    def pack_slab_cap(self, points_ptr, desc_ptr, counts_ptr, nframes, slab_ptr, cap_bytes) -> None:
+        """Pack into a buffer of a capacity agreed once (no host sync); a batch
+        that does not fit sets SLAB_OVERFLOW in the slab's flags."""
+        check(_lib.surfhip_pack_slab_cap(self.h, points_ptr, desc_ptr, counts_ptr, nframes, slab_ptr, cap_bytes),
+              "pack_slab_cap")
+
     def detect(self, image_ptr: int, pitch: int, points_ptr: int, max_pts: int, desc: bool = True):
         """Surfor::detectAndCompute semantics for one frame (synchronous)."""
         n = C.c_int()
@@ -475,6 +482,13 @@ def downsample2(img: np.ndarray, w: int, h: int) -> np.ndarray:
     return out
 
 
+SLAB_TRUNCATED, SLAB_OVERFLOW = 1, 2      # slab header flags (include/surfhip.h)
+
+
+def slab_flags(buf: np.ndarray) -> int:
+    return int(np.ascontiguousarray(buf[:16]).view(np.uint8).view(np.int32)[3])
+
+
 def parse_slab(buf: np.ndarray):
     """Host view of one compacted result slab (see include/surfhip.h):
     returns (counts[nframes], points[total], desc[total, nf] or None)."""
@@ -502,6 +516,68 @@ def build_slab(counts: np.ndarray, pts: np.ndarray, desc) -> np.ndarray:
     if nf:
         out[head + 48 * total:] = np.ascontiguousarray(desc[:total], dtype=np.float32).view(np.uint8).ravel()
     return out
+
+
+# ------------------------------------------------------ multi-GPU exchange
+
+COMM_PATH = os.path.join(_HERE, "libsurfcomm.so")
+COMM_ID_BYTES = 128
+_comm_lib = None
+
+
+def _comm():
+    """libsurfcomm.so (include/surfhip_comm.h), loaded on first use so that
+    single-GPU callers never load RCCL."""
+    global _comm_lib
+    if _comm_lib is None:
+        if not os.path.exists(COMM_PATH):
+            raise ImportError(f"surf_amd: {COMM_PATH} is missing -- run `make -C cuda-surf_amd`")
+        L = C.CDLL(COMM_PATH)
+        for name, res, args in (("surfhip_comm_unique_id", _i, [_vp]),
+                                ("surfhip_comm_init", _i, [C.POINTER(_vp), _i, _i, _vp]),
+                                ("surfhip_comm_destroy", _i, [_vp]),
+                                ("surfhip_comm_rank", _i, [_vp, C.POINTER(_i), C.POINTER(_i)]),
+                                ("surfhip_allgather", _i, [_vp, _vp, _sz, _vp, _vp]),
+                                ("surfhip_allreduce_sum_i64", _i, [_vp, _vp, _i, _vp]),
+                                ("surfhip_comm_last_error", _i, [])):
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        _comm_lib = L
+    return _comm_lib
+
+
+def comm_unique_id() -> bytes:
+    buf = C.create_string_buffer(COMM_ID_BYTES)
+    rc = _comm().surfhip_comm_unique_id(buf)
+    check(rc, f"comm_unique_id (rccl {_comm().surfhip_comm_last_error()})")
+    return buf.raw
+
+
+class Comm:
+    """One RCCL communicator of this process's GPU (surfhip_comm_*).  The
+    128-byte id comes from comm_unique_id() on one rank, shared out of band
+    (the bench broadcasts it over its torch.distributed group)."""
+
+    def __init__(self, nranks: int, rank: int, uid: bytes):
+        assert len(uid) == COMM_ID_BYTES
+        h = C.c_void_p()
+        idb = C.create_string_buffer(uid, COMM_ID_BYTES)
+        rc = _comm().surfhip_comm_init(C.byref(h), nranks, rank, idb)
+        check(rc, f"comm_init (rccl {_comm().surfhip_comm_last_error()})")
+        self.h, self.nranks, self.rank = h.value, nranks, rank
+
+    def allgather(self, send_ptr: int, nbytes: int, recv_ptr: int, stream=None) -> None:
+        rc = _comm().surfhip_allgather(self.h, send_ptr, nbytes, recv_ptr, stream)
+        check(rc, f"allgather (rccl {_comm().surfhip_comm_last_error()})")
+
+    def allreduce_sum_i64(self, ptr: int, n: int, stream=None) -> None:
+        rc = _comm().surfhip_allreduce_sum_i64(self.h, ptr, n, stream)
+        check(rc, f"allreduce (rccl {_comm().surfhip_comm_last_error()})")
+
+    def close(self) -> None:
+        if self.h:
+            _comm().surfhip_comm_destroy(self.h)
+            self.h = None
 
 
 class Ingest:

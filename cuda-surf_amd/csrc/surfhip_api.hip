@@ -723,13 +723,20 @@ int surfhip_batch_total(surfhip_detector* d, int nframes, int* total)
     return SURFHIP_OK;
 }
 
+int surfhip_pack_slab_cap(surfhip_detector* d, const surfhip_point* pts, const float* desc, const int* counts,
+                          int nframes, void* slab, size_t cap_bytes)
+{
+    if (!d || !pts || !counts || !slab || nframes < 1 || nframes > d->max_batch) return SURFHIP_ERR_INVALID;
+    if (cap_bytes < surfhip_slab_bytes(nframes, 0, 0)) return SURFHIP_ERR_INVALID;
+    HIPCHK(launch_pack(pts, desc, counts, d->offsets, nframes, d->max_pts, d->param.nfeatures, d->status, cap_bytes,
+                       (uint8_t*)slab, d->stream));
+    return SURFHIP_OK;
+}
+
 int surfhip_pack_slab(surfhip_detector* d, const surfhip_point* pts, const float* desc, const int* counts,
                       int nframes, void* slab)
 {
-    if (!d || !pts || !counts || !slab || nframes < 1 || nframes > d->max_batch) return SURFHIP_ERR_INVALID;
-    HIPCHK(launch_pack(pts, desc, counts, d->offsets, nframes, d->max_pts, d->param.nfeatures, d->status, (uint8_t*)slab,
-                       d->stream));
-    return SURFHIP_OK;
+    return surfhip_pack_slab_cap(d, pts, desc, counts, nframes, slab, (size_t)-1);
 }
 
 size_t surfhip_match_scratch(int n1, int n2, int flags)

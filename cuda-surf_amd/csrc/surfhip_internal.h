@@ -129,6 +129,7 @@ size_t match_scratch_bytes(int n1, int n2, int flags);
 hipError_t launch_match(surfhip_point* pts1, const surfhip_point* pts2, const float* f1, const float* f2, int n1,
                         int n2, int nf, int flags, void* scratch, hipStream_t s);
 hipError_t launch_pack(const surfhip_point* pts, const float* desc, const int* counts, const int* offsets,
-                       int nframes, int max_pts, int nfeat, const int* status, uint8_t* slab, hipStream_t s);
+                       int nframes, int max_pts, int nfeat, const int* status, size_t cap_bytes, uint8_t* slab,
+                       hipStream_t s);
 
 }  // namespace surfhip

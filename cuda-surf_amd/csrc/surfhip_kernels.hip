@@ -3009,18 +3009,27 @@ hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_poin
 __global__ __launch_bounds__(256) void k_pack(const surfhip_point* __restrict__ pts, const float* __restrict__ desc,
                                               const int* __restrict__ counts, const int* __restrict__ offsets,
                                               int nframes, int max_pts, int nfeat, const int* __restrict__ status,
-                                              uint8_t* __restrict__ slab)
+                                              size_t cap_bytes, uint8_t* __restrict__ slab)
 {
     const int f = blockIdx.y;
     const int total = offsets[nframes];
+    const size_t head = 16 + (((size_t)nframes * 4 + 15) & ~(size_t)15);
+    const size_t need = head + (size_t)total * (sizeof(surfhip_point) + (desc ? 4 * (size_t)nfeat : 0));
+    const bool fits = need <= cap_bytes;
     int* hdr = reinterpret_cast<int*>(slab);
     if (f == 0 && blockIdx.x == 0) {
-        // hdr[3] bit 0: a frame of this batch was truncated at the candidate capacity
-        if (threadIdx.x == 0) { hdr[0] = nframes; hdr[1] = total; hdr[2] = desc ? nfeat : 0; hdr[3] = status ? (*status & 1) : 0; }
+        // hdr[3] bit 0: a frame of this batch was truncated at the candidate
+        // capacity; bit 1: the slab did not fit cap_bytes (payload not written)
+        if (threadIdx.x == 0) {
+            hdr[0] = nframes;
+            hdr[1] = total;
+            hdr[2] = desc ? nfeat : 0;
+            hdr[3] = (status ? (*status & 1) : 0) | (fits ? 0 : 2);
+        }
         const int npad = (nframes + 3) & ~3;          // counts padded to 16 B with zeros (stable file bytes)
         for (int i = threadIdx.x; i < npad; i += 256) hdr[4 + i] = i < nframes ? counts[i] : 0;
     }
-    const size_t head = 16 + (((size_t)nframes * 4 + 15) & ~(size_t)15);
+    if (!fits) return;
     surfhip_point* pout = reinterpret_cast<surfhip_point*>(slab + head);
     float* dout = reinterpret_cast<float*>(slab + head + (size_t)total * sizeof(surfhip_point));
     const int cnt = counts[f], off = offsets[f];
@@ -3036,9 +3045,11 @@ __global__ __launch_bounds__(256) void k_pack(const surfhip_point* __restrict__ 
 }
 
 hipError_t launch_pack(const surfhip_point* pts, const float* desc, const int* counts, const int* offsets,
-                       int nframes, int max_pts, int nfeat, const int* status, uint8_t* slab, hipStream_t s)
+                       int nframes, int max_pts, int nfeat, const int* status, size_t cap_bytes, uint8_t* slab,
+                       hipStream_t s)
 {
-    k_pack<<<dim3(16, nframes), 256, 0, s>>>(pts, desc, counts, offsets, nframes, max_pts, nfeat, status, slab);
+    k_pack<<<dim3(16, nframes), 256, 0, s>>>(pts, desc, counts, offsets, nframes, max_pts, nfeat, status,
+                                             cap_bytes, slab);
     return hipGetLastError();
 }
 

@@ -187,7 +187,8 @@ long long surfhip_hessian_bytes_per_frame(surfhip_detector* det);
 /* Result slab for the multi-GPU all-gather, compacted to the
  * keypoints actually found by the last detect_batch:
  *   int32 {nframes, total, nfeatures (0 without descriptors), flags}
- *     (flags bit 0: a frame was truncated at the candidate capacity)
+ *     (flags bit 0: a frame was truncated at the candidate capacity;
+ *      bit 1: the slab exceeded surfhip_pack_slab_cap's capacity)
  *   int32 counts[nframes] padded to 16 B
  *   SurfPoint points[total]          (frame-major, canonical order)
  *   float desc[total][nfeatures]
@@ -197,6 +198,13 @@ size_t surfhip_slab_bytes(int nframes, int total, int nfeatures);
 int surfhip_batch_total(surfhip_detector* det, int nframes, int* total);
 int surfhip_pack_slab(surfhip_detector* det, const surfhip_point* d_points, const float* d_desc,
                       const int* d_counts, int nframes, void* d_slab);
+/* The same into a buffer of cap_bytes, with no host synchronisation: the
+ * multi-GPU path sizes every rank's slab once (a per-frame keypoint budget,
+ * SURVEY.md 8e) and all-gathers that many bytes per batch.  A batch that
+ * does not fit writes its header and counts with flags bit 1 set and no
+ * payload; the receiver must check the flags. */
+int surfhip_pack_slab_cap(surfhip_detector* det, const surfhip_point* d_points, const float* d_desc,
+                          const int* d_counts, int nframes, void* d_slab, size_t cap_bytes);
 
 /* ------------------------------------------------------------ matching --
  * Surfor::match (surf.cpp:418-428) -> cuFindMaxCorr (surfd.cu:3554-3566) ->

@@ -39,6 +39,19 @@ def test_surfhip_exports_every_declared_symbol(surf):
         getattr(surf.lib, n)
 
 
+def test_surfcomm_exports_every_declared_symbol():
+    """libsurfcomm.so (RCCL exchange of packed slabs, include/surfhip_comm.h)
+    exports every declared entry point; no GPU call is made."""
+    lib = os.path.join(PKG, "libsurfcomm.so")
+    if not os.path.exists(lib):
+        subprocess.check_call(["make", "-s", "-C", PKG, "libsurfcomm.so"])
+    names = declared_functions("surfhip_comm.h")
+    assert len(names) >= 6
+    syms = exported(lib)
+    missing = [n for n in names if not re.search(rf"\bT {n}$", syms, flags=re.M)]
+    assert not missing, missing
+
+
 def test_libsurf_exports_reference_api():
     lib = os.path.join(PKG, "libsurf.so")
     if not os.path.exists(lib):
