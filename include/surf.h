@@ -23,7 +23,9 @@ namespace surf
         Surfor();
         ~Surfor();
 
-        /* Parameters (surf.h:27-29 of the reference); doubled=true is not supported. */
+        /* Parameters (surf.h:27-29 of the reference); doubled=true upsamples the
+         * frame 2x before the integral (surf.cpp:234, 377-378) and describes at
+         * (2x, 2y), 3.3*scale (surfd.cu:1581-1592). */
         void init(const int _noctaves, const float _thresh = 0.2f, const bool _doubled = false,
                   const int _init_mask_size = 9, const int _sampling_step = 2, const bool _upright = false,
                   const bool _extend = false, const int _desc_wsz = 4, const int _width = -1,

@@ -34,7 +34,8 @@ def _free_port():
 
 
 def test_comm_single_rank_allgather(surf):
-    import torch  # noqa: F401  (one HIP runtime: torch's)
+    """In the test process (no torch: one HIP runtime, /opt/rocm's) libsurfcomm
+    resolves /opt/rocm's RCCL; under torch it binds torch's bundled copy."""
     w, h, n = 640, 480, 3
     frames = surf.synth_frames(n, w, h, first=11)
     param = surf.make_param(4, 4.0, upright=True)
@@ -121,7 +122,7 @@ def _worker(rank, world, port, n_frames, w, h, q):
 
 
 def test_two_ranks_product_slabs_gloo(surf, orc):
-    import torch.multiprocessing as mp
+    import multiprocessing as mp                    # not torch's: the test process stays torch-free
 
     world, n_frames, w, h = 2, 5, 640, 480
     ctx = mp.get_context("spawn")
@@ -168,3 +169,29 @@ def test_bench_world2_loop_gloo_rehearsal():
     assert d["n_gpus"] == 2 and d["value"] > 0
     ex = d["exchange"]
     assert ex["backend"] == "gloo" and ex["keypoints_gathered_per_step"] == d["keypoints_per_step"] > 0
+
+
+_UNDER_TORCH = r"""
+import importlib.util, sys
+import torch
+spec = importlib.util.spec_from_file_location("surf_amd", sys.argv[1] + "/cuda-surf_amd/__init__.py",
+                                              submodule_search_locations=[sys.argv[1] + "/cuda-surf_amd"])
+surf = importlib.util.module_from_spec(spec); sys.modules["surf_amd"] = surf; spec.loader.exec_module(surf)
+dev = torch.device("cuda", 0)
+s = torch.cuda.Stream(dev)
+comm = surf.Comm(1, 0, surf.comm_unique_id())
+src = torch.arange(1 << 20, dtype=torch.int32, device=dev).view(torch.uint8)
+dst = torch.zeros_like(src)
+comm.allgather(src.data_ptr(), src.numel(), dst.data_ptr(), s.cuda_stream)
+s.synchronize()
+assert torch.equal(src, dst)
+comm.close()
+print("UNDER_TORCH_OK")
+"""
+
+
+def test_comm_under_torch():
+    """bench.py's arrangement: torch loaded first, so libsurfcomm binds the
+    RCCL and HIP runtime torch bundles (one copy of each in the process)."""
+    r = subprocess.run([sys.executable, "-c", _UNDER_TORCH, REPO], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0 and "UNDER_TORCH_OK" in r.stdout, r.stderr[-3000:]

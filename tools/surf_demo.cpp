@@ -1,7 +1,11 @@
 // surf_demo.cpp -- the reference's main.cpp flow (cudaSurfDemo2,
 // main.cpp:163-283) against this engine's drop-in headers, minus OpenCV:
 // images come from a PGM reader instead of cv::imread and nothing is drawn.
-// Usage: surf_demo [device] [left.pgm] [right.pgm] [repeats]
+// Usage: surf_demo [device] [left.pgm] [right.pgm] [repeats] [dump_prefix]
+// With dump_prefix, writes <prefix>_left.bin / _right.bin (after detection)
+// and <prefix>_match.bin (set 1 after match): int32 n, int32 nfeatures, then
+// n SurfPoints (h_data) and n x nfeatures descriptor floats (none in _match).
+#include <cstdio>
 #include <memory>
 #include <vector>
 
@@ -20,12 +24,32 @@ static bool load(const char* path, std::vector<uchar>& px, int& w, int& h)
     return surf_pgm_read(path, px.data(), w) == 0;
 }
 
+static bool dump(const char* prefix, const char* tag, const surf::SurfData& d, const float* d_desc, int nf)
+{
+    char path[1024];
+    snprintf(path, sizeof path, "%s_%s.bin", prefix, tag);
+    FILE* f = fopen(path, "wb");
+    if (!f) return false;
+    const int hdr[2] = {d.num_pts, d_desc ? nf : 0};
+    bool ok = fwrite(hdr, sizeof hdr, 1, f) == 1;
+    if (d.num_pts > 0)
+        ok = ok && fwrite(d.h_data, sizeof(surf::SurfPoint), d.num_pts, f) == (size_t)d.num_pts;
+    if (d_desc && d.num_pts > 0)
+    {
+        std::vector<float> h((size_t)d.num_pts * nf);
+        CHECK(cudaMemcpy(h.data(), d_desc, h.size() * sizeof(float), cudaMemcpyDeviceToHost));
+        ok = ok && fwrite(h.data(), sizeof(float), h.size(), f) == h.size();
+    }
+    return fclose(f) == 0 && ok;
+}
+
 int main(int argc, char** argv)
 {
     const int devNum = argc > 1 ? atoi(argv[1]) : 0;
     const char* lpath = argc > 2 ? argv[2] : "data/left.pgm";
     const char* rpath = argc > 3 ? argv[3] : "data/right.pgm";
     const int nrepeats = argc > 4 ? atoi(argv[4]) : 100;
+    const char* prefix = argc > 5 ? argv[5] : nullptr;
 
     std::vector<uchar> limg, rimg;
     int lw, lh, rw, rh;
@@ -78,12 +102,26 @@ int main(int argc, char** argv)
         detector->detectAndCompute(img2, surf_data2, whp2, &surf_descriptors2, true);
     }
     float t2 = timer.read();
+    const int nf = 16 * indexSize * indexSize / 4 * (extended ? 2 : 1);
+    if (prefix && !(dump(prefix, "left", surf_data1, surf_descriptors1, nf) &&
+                    dump(prefix, "right", surf_data2, surf_descriptors2, nf)))
+    {
+        fprintf(stderr, "cannot write %s_*.bin\n", prefix);
+        return 1;
+    }
+    // main.cpp:248-251
+    for (int i = 0; i < nrepeats; i++)
+        detector->match(surf_data1, surf_data2, surf_descriptors1, surf_descriptors2);
+    float t3 = timer.read();
+    if (prefix && !dump(prefix, "match", surf_data1, nullptr, nf))
+        return 1;
 
     std::cout << "Number of features1: " << surf_data1.num_pts << std::endl
               << "Number of features2: " << surf_data2.num_pts << std::endl;
     std::cout << "Time for allocating image memory:  " << t0 << std::endl
               << "Time for allocating point memory:  " << t1 - t0 << std::endl
-              << "Time of detection and computation: " << (t2 - t1) / nrepeats << std::endl;
+              << "Time of detection and computation: " << (t2 - t1) / nrepeats << std::endl
+              << "Time of matching surf keypoints:   " << (t3 - t2) / nrepeats << std::endl;
     for (int i = 0; i < std::min(3, surf_data1.num_pts); i++)
     {
         const surf::SurfPoint& p = surf_data1.h_data[i];
