@@ -59,7 +59,9 @@ STAGES = ("integral", "hessian", "nms", "sort", "describe", "total")
 
 # ------------------------------------------------------------------ library
 
-LIB_PATH = os.path.join(_HERE, "libsurfhip.so")
+# SURFHIP_LIB_DIR: a directory holding an alternative build of libsurfhip.so
+# (diagnostic kernel variants, tools/diag_build.sh); the default is in-tree.
+LIB_PATH = os.path.join(os.environ.get("SURFHIP_LIB_DIR") or _HERE, "libsurfhip.so")
 SYNTH_PATH = os.path.join(_HERE, "libsurfsynth.so")
 
 # The HIP runtime must be a single copy per process: if PyTorch is already

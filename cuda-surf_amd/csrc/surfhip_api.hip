@@ -457,7 +457,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     ALLOC(d->item_off, (2 * B * (size_t)d->nitems + 64) * sizeof(int));
     ALLOC(d->offsets, (B + 1) * sizeof(int));
     ALLOC(d->order, B * (size_t)max_pts * sizeof(int));
-    ALLOC(d->status, 16);
+    ALLOC(d->status, 256 + kDescQueueBytes);    // [0]: flags; from [64]: describe work queues
     ALLOC(d->pts1, (size_t)max_pts * sizeof(surfhip_point));
     ALLOC(d->desc1, (size_t)max_pts * d->param.nfeatures * sizeof(float));
     ALLOC(d->count1, 16);
@@ -603,7 +603,8 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
                        d->cap, nframes, points, d->max_pts, counts, d->offsets, d->order, d->status, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[4], s));
     if (desc)
-        HIPCHK(launch_describe(d->ii, d->P, points, d->max_pts, counts, d->offsets, d->order, nframes, desc, s));
+        HIPCHK(launch_describe(d->ii, d->P, points, d->max_pts, counts, d->offsets, d->order, nframes, desc,
+                               d->status + 64, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[5], s));
     d->last_nframes = nframes;
     d->last_frames = frames;

@@ -19,6 +19,8 @@ constexpr int kMaxOct = 8;
 constexpr int kMaxScale = 8;
 constexpr int kSortCap = 16384;     // candidates per frame sorted in LDS
 constexpr uint32_t kNoKey = 0xffffffffu;   // candidate slot of a rejected NMS survivor
+constexpr int kDescQ = 16;                  // describe work queues per XCD
+constexpr int kDescQueueBytes = 8 * kDescQ * 64 * 4;
 constexpr int kBandRows = 32;       // integral-image band height
 constexpr int kScanRows = 16;       // NMS block rows per scan workgroup (4 per wave)
 constexpr int kItemCap = 64 * (kScanRows / 4);   // 2x2x2 blocks (= survivor slots) per scan item
@@ -117,9 +119,11 @@ hipError_t launch_sort(const surfhip_point* cand, const uint32_t* keys, uint64_t
                        surfhip_point* out, int max_pts, int* out_count, int* offsets, int* order, int* status,
                        hipStream_t s);
 hipError_t set_max_lds(const void* fn, int bytes);
+// queue: kDescQueueBytes of device scratch (the per-XCD work counters of
+// k_describe_ur, 8 x kDescQ of them 256 B apart, zeroed by the launch)
 hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
                            const int* counts, const int* offsets, const int* order, int nframes, float* desc,
-                           hipStream_t s);
+                           int* queue, hipStream_t s);
 // Doubled-image input (surfhip_double.hip): frames (W x H) -> D ((2W-2) x
 // (2H-2) u8, row pitch dpitch, a multiple of 4).
 hipError_t launch_double(const uint8_t* frames, int pitch, long long fstride, int nframes, int W, int H,

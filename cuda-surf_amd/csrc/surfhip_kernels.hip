@@ -134,6 +134,15 @@ __device__ __forceinline__ void buf_st_nt(rsrc_t r, uint32_t off, float v)
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 2);
 }
 
+// LDS ordering between the lanes of one wave, no wait: the LDS executes one
+// wave's DS instructions in issue order, so a ds_read issued after a
+// ds_write of the same wave sees it (and a later write cannot overtake an
+// earlier read); only the compiler must keep the order.
+__device__ __forceinline__ void lds_order()
+{
+    asm volatile("" ::: "memory");
+}
+
 // LDS visibility between the lanes of one wave
 __device__ __forceinline__ void wave_sync()
 {
@@ -1836,9 +1845,33 @@ __global__ __launch_bounds__(1024) void k_sort(const surfhip_point* __restrict__
         out[(size_t)f * max_pts + t] = cand[(size_t)f * cap + (uint32_t)(s[t] & 0xffffffffu)];
     if (threadIdx.x == 0) out_count[f] = keep;
     // Describe schedule (processing order only; descriptors land at their
-    // canonical index).  Canonical order: row-ordered schedules measured no
-    // faster (the descriptor is bound by texture-address work, not L2).
-    for (int t = threadIdx.x; t < keep; t += blockDim.x) order[(size_t)f * max_pts + t] = t;
+    // canonical index): keypoints in 16-row bands of the frame, canonical
+    // order within a band.  The canonical order sweeps the frame 2 x noctaves
+    // times (octave, layer, y); the band order sweeps it once, so the few
+    // hundred keypoints an XCD describes at a time share their integral-image
+    // rows in that XCD's L2.
+    int* ord = order + (size_t)f * max_pts;
+    int nb = 1;
+    while (nb < keep) nb <<= 1;
+    if (nb > 2 * kSortCap) {
+        for (int t = threadIdx.x; t < keep; t += blockDim.x) ord[t] = t;
+        return;
+    }
+    __threadfence_block();
+    __syncthreads();                          // s[] is dead, out[] is written
+    uint32_t* bk = reinterpret_cast<uint32_t*>(sk);
+    for (int t = threadIdx.x; t < nb; t += blockDim.x) {
+        uint32_t k = 0xffffffffu;
+        if (t < keep) {
+            const float y = out[(size_t)f * max_pts + t].y;
+            const uint32_t band = min((uint32_t)max(y, 0.f) >> 4, 4095u);
+            k = (band << 20) | (uint32_t)t;
+        }
+        bk[t] = k;
+    }
+    __syncthreads();
+    bitonic_sort(bk, nb);
+    for (int t = threadIdx.x; t < keep; t += blockDim.x) ord[t] = (int)(bk[t] & 0xfffffu);
 }
 
 __global__ __launch_bounds__(1024) void k_offsets(const int* __restrict__ counts, int nframes, int* __restrict__ offsets)
@@ -2480,6 +2513,25 @@ __device__ __forceinline__ uint32_t bld(__amdgpu_buffer_rsrc_t r, int off)
     return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
 }
 
+template <int NS>
+__device__ __forceinline__ void haar_bins(int32_t wav1, int32_t wav2, float weight, bool ok, float (&S)[NS])
+{
+    // {dx, dy} = weight * {wav2, wav1} in one packed multiply; a lane
+    // outside the grid contributes 0 (a select: its inputs may be garbage)
+    v2f32 d = v2f32{(float)wav2, (float)wav1} * weight;
+    const float dx = ok ? d.x : 0.f, dy = ok ? d.y : 0.f;
+    if constexpr (NS == 4) {
+        S[0] = dx; S[1] = fminf(dx, 0.f);          // bins 1 | 0 by sign of dx
+        S[2] = dy; S[3] = fminf(dy, 0.f);          // bins 3 | 2 by sign of dy
+    } else {
+        const float adx = fabsf(dx), ady = fabsf(dy);
+        S[0] = dx;  S[1] = dy < 0.f ? dx : 0.f;    // bins 1 | 0 by sign of dy
+        S[2] = adx; S[3] = dy < 0.f ? adx : 0.f;   // bins 3 | 2
+        S[4] = dy;  S[5] = dx < 0.f ? dy : 0.f;    // bins 5 | 4 by sign of dx
+        S[6] = ady; S[7] = dx < 0.f ? ady : 0.f;   // bins 7 | 6
+    }
+}
+
 template <int R> struct IntC { static constexpr int value = R; };
 
 template <bool EXT>
@@ -2487,7 +2539,7 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
                                                      const surfhip_point* __restrict__ pts, int max_pts,
                                                      const int* __restrict__ offsets,
                                                      const int* __restrict__ order, int nframes,
-                                                     float* __restrict__ desc)
+                                                     float* __restrict__ desc, int* __restrict__ queue)
 {
     constexpr int WSZ = 4;
     constexpr int NB = EXT ? 8 : 4;                       // bins per cell
@@ -2499,26 +2551,40 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
     __shared__ int s_ri[4][64];
     __shared__ float4 s_wr[4][64];               // per grid row: weights of cell rows 0..3
     __shared__ __attribute__((aligned(16))) uint32_t s_seg[4][448];   // segment path: the wave's integral rows
-    __shared__ unsigned long long s_mask[4][6];
+    __shared__ int4 s_run[4][6];
+    // Gaussian weights premultiplied by 1/255 (the reference scales the Haar
+    // response by the weight, then by 1/255: one rounding moves, within the
+    // descriptor tolerance)
     __shared__ float s_lut[40];
-    if (threadIdx.x < 40) s_lut[threadIdx.x] = c_tab.lut2[threadIdx.x];
+    if (threadIdx.x < 40) s_lut[threadIdx.x] = c_tab.lut2[threadIdx.x] * INV255;
     __syncthreads();
     const int lane = (int)lane_id();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);     // wave-uniform: SGPR descriptors
     const int total = offsets[nframes];
     const float fw = (float)WSZ;
     const float wofs = (float)WSZ * 0.5f - 0.5f;
-    // XCD-aware split: the workgroups of one XCD (blockIdx % 8) take one
-    // contiguous eighth of the keypoints, i.e. a few whole frames, so the
-    // integral-image patches they gather stay in that XCD's L2.
-    const int xcd = blockIdx.x & 7, nbx = gridDim.x >> 3, lb = blockIdx.x >> 3;
+    // XCD-aware work queues: the workgroups of one XCD (blockIdx % 8) take one
+    // contiguous eighth of the keypoints (a few whole frames, each in the
+    // band order k_sort writes), one keypoint per grab, so the keypoints in
+    // flight on an XCD are consecutive -- a band of a frame whose
+    // integral-image rows stay in that XCD's L2.  The eighth is dealt
+    // round-robin over kDescQ counters (keypoint gbeg + kDescQ g + q), each
+    // on its own 256-B line: one same-address atomic per keypoint would
+    // serialise the XCD at ~50 cycles a grab.
+    const int xcd = blockIdx.x & 7;
     const int chunk = (total + 7) >> 3;
     const int gbeg = xcd * chunk, gend = min(total, gbeg + chunk);
+    const int qi = ((blockIdx.x >> 3) * 4 + w) % kDescQ;
+    int* qctr = queue + (xcd * kDescQ + qi) * 64;
+    auto grab = [&]() {
+        int g = 0;
+        if (lane == 0) g = atomicAdd(qctr, 1);
+        return gbeg + kDescQ * __builtin_amdgcn_readfirstlane(g) + qi;
+    };
     // the wave's keypoints ascend, so its frame is tracked incrementally
     // (one binary search per wave) and the next keypoint is fetched while
     // the current one is described
-    const int gstride = nbx * 4;
-    int gn = gbeg + lb * 4 + w;
+    int gn = grab();
     int fn = 0, fnb = 0, fne = 0, kn = 0;
     surfhip_point pn;
     if (gn < gend) {
@@ -2536,7 +2602,7 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
     while (gn < gend) {
         const int f = fn, kp = kn;
         const surfhip_point p = pn;
-        gn += gstride;
+        gn = grab();
         if (gn < gend) {
             while (gn >= fne) { fn++; fnb = fne; fne = offsets[fn + 1]; }
             kn = order[(size_t)fn * max_pts + (gn - fnb)];
@@ -2617,20 +2683,8 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
             // r+s+1 (a0*, a1*, a2*, a3*), cols c-s, c+s+1, c, c+1
             const int32_t wav1 = (int32_t)((a21 + a00 - a01 - a20) - (a31 + a10 - a11 - a30));
             const int32_t wav2 = (int32_t)((a31 + a02 - a01 - a32) - (a33 + a00 - a03 - a30));
-            const float weight = s_lut[f2i_rz(rp + cp2)];
-            const float dx = (weight * (float)wav2) * INV255;
-            const float dy = (weight * (float)wav1) * INV255;
             float S[NS];
-            if constexpr (!EXT) {
-                S[0] = dx; S[1] = fminf(dx, 0.f);          // bins 1 | 0 by sign of dx
-                S[2] = dy; S[3] = fminf(dy, 0.f);          // bins 3 | 2 by sign of dy
-            } else {
-                const float adx = fabsf(dx), ady = fabsf(dy);
-                S[0] = dx;  S[1] = dy < 0.f ? dx : 0.f;    // bins 1 | 0 by sign of dy
-                S[2] = adx; S[3] = dy < 0.f ? adx : 0.f;   // bins 3 | 2
-                S[4] = dy;  S[5] = dx < 0.f ? dy : 0.f;    // bins 5 | 4 by sign of dx
-                S[6] = ady; S[7] = dx < 0.f ? ady : 0.f;   // bins 7 | 6
-            }
+            haar_bins(wav1, wav2, s_lut[f2i_rz(rp + cp2)], true, S);
             const float w0 = 1.f - rf;
             // the cell row is uniform over the wave except where the two
             // halves (dual mode) straddle a cell-row boundary
@@ -2727,6 +2781,7 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
                                       const uint32_t (&Nv)[8]) {
                         const int t = t0 + hh + 2 * n;
                         if (!(col_on && n < nstep)) return;
+                        constexpr bool ok = true;
 #ifdef SURF_DIAG_NOCOMP
                         acc[0][0] += (float)(Pv[0] ^ Cv[3] ^ Nv[5] ^ Pv[7] ^ Nv[1]);
                         return;
@@ -2743,20 +2798,8 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
                         // haarX / haarY (surfd.cu:1171-1182 via getSum)
                         const int32_t wav1 = (int32_t)((a21 + a00 - a01 - a20) - (a31 + a10 - a11 - a30));
                         const int32_t wav2 = (int32_t)((a31 + a02 - a01 - a32) - (a33 + a00 - a03 - a30));
-                        const float weight = s_lut[f2i_rz(rp + cp2)];
-                        const float dx = (weight * (float)wav2) * INV255;
-                        const float dy = (weight * (float)wav1) * INV255;
                         float S[NS];
-                        if constexpr (!EXT) {
-                            S[0] = dx; S[1] = fminf(dx, 0.f);          // bins 1 | 0 by sign of dx
-                            S[2] = dy; S[3] = fminf(dy, 0.f);          // bins 3 | 2 by sign of dy
-                        } else {
-                            const float adx = fabsf(dx), ady = fabsf(dy);
-                            S[0] = dx;  S[1] = dy < 0.f ? dx : 0.f;    // bins 1 | 0 by sign of dy
-                            S[2] = adx; S[3] = dy < 0.f ? adx : 0.f;   // bins 3 | 2
-                            S[4] = dy;  S[5] = dx < 0.f ? dy : 0.f;    // bins 5 | 4 by sign of dx
-                            S[6] = ady; S[7] = dx < 0.f ? ady : 0.f;   // bins 7 | 6
-                        }
+                        haar_bins(wav1, wav2, s_lut[f2i_rz(rp + cp2)], ok, S);
                         // all four cell rows with the row's weights (two are 0):
                         // branch-free, fixed registers
                         const float wrr[WSZ] = {wr.x, wr.y, wr.z, wr.w};
@@ -2835,12 +2878,12 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
                 auto proc = [&](const Seg& q, uint32_t (&T)[8]) {
                     if (cok[0]) *reinterpret_cast<uint4*>(buf + cdst[0]) = q.c0;
                     if (cok[1]) *reinterpret_cast<uint4*>(buf + cdst[1]) = q.c1;
-                    wave_sync();
+                    lds_order();
                     const uint32_t* r0 = buf + rowg + xo;
                     const uint32_t* r1 = r0 + WP;
                     T[0] = r0[-hs]; T[1] = r0[0]; T[2] = r0[1]; T[3] = r0[hs + 1];
                     T[4] = r1[-hs]; T[5] = r1[0]; T[6] = r1[1]; T[7] = r1[hs + 1];
-                    wave_sync();
+                    lds_order();
                 };
                 (void)gstride;
                 for (int ph = 0; ph < (dual ? 1 : 2); ph++) {
@@ -2855,6 +2898,11 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
                                       const uint32_t (&Nv)[8]) {
                         const int t = t0 + hh + 2 * n;
                         if (!(col_on && n < nstep)) return;
+                        constexpr bool ok = true;
+#ifdef SURF_DIAG_NOCOMP
+                        acc[0][0] += (float)(Pv[0] ^ Cv[3] ^ Nv[5] ^ Pv[7] ^ Nv[1]);
+                        return;
+#endif
                         const float rp = s_rp[w][t];
                         const float4 wr = s_wr[w][t];
                         const uint32_t a00 = A ? Pv[0] : Pv[4], a02 = A ? Pv[1] : Pv[5];
@@ -2864,20 +2912,8 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
                         const uint32_t a10 = Cv[0], a11 = Cv[3], a20 = Cv[4], a21 = Cv[7];
                         const int32_t wav1 = (int32_t)((a21 + a00 - a01 - a20) - (a31 + a10 - a11 - a30));
                         const int32_t wav2 = (int32_t)((a31 + a02 - a01 - a32) - (a33 + a00 - a03 - a30));
-                        const float weight = s_lut[f2i_rz(rp + cp2)];
-                        const float dx = (weight * (float)wav2) * INV255;
-                        const float dy = (weight * (float)wav1) * INV255;
                         float S[NS];
-                        if constexpr (!EXT) {
-                            S[0] = dx; S[1] = fminf(dx, 0.f);
-                            S[2] = dy; S[3] = fminf(dy, 0.f);
-                        } else {
-                            const float adx = fabsf(dx), ady = fabsf(dy);
-                            S[0] = dx;  S[1] = dy < 0.f ? dx : 0.f;
-                            S[2] = adx; S[3] = dy < 0.f ? adx : 0.f;
-                            S[4] = dy;  S[5] = dx < 0.f ? dy : 0.f;
-                            S[6] = ady; S[7] = dx < 0.f ? ady : 0.f;
-                        }
+                        haar_bins(wav1, wav2, s_lut[f2i_rz(rp + cp2)], ok, S);
                         const float wrr[WSZ] = {wr.x, wr.y, wr.z, wr.w};
 #pragma unroll
                         for (int R = 0; R < WSZ; R++)
@@ -2892,6 +2928,9 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
                         proc(q1, Y);
                     }
                     Seg s0 = ldseg(pb + 2), s1 = ldseg(pb + 4), s2 = ldseg(pb + 6);
+#ifdef SURF_DIAG_NOROWS
+                    continue;
+#endif
                     for (int n = 0; n < nmax; n += 3) {
                         const int tt = pb + 2 * n;
                         proc(s0, Z);
@@ -2936,10 +2975,16 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
                 red[w][lane][R * NB + 2 * q + 1] = acc[R][2 * q] - acc[R][2 * q + 1];
             }
         s_cf[w][lane] = cfrac;
+        // The lanes of one cell column (ci == C) are one contiguous run per
+        // half (cx and the image-bounds test are monotonic in j); the run's
+        // [lo, hi) per half goes to s_run[C + 1] = {lo0, hi0, lo1, hi1}.
 #pragma unroll
         for (int C = -1; C < WSZ; C++) {
             const unsigned long long mc = __ballot(col_on && ci == C);
-            if (lane == 0) s_mask[w][C + 1] = mc;
+            const uint32_t mlo = (uint32_t)mc, mhi = (uint32_t)(mc >> 32);
+            if (lane == 0)
+                s_run[w][C + 1] = make_int4(mlo ? __builtin_ctz(mlo) : 0, mlo ? 32 - __builtin_clz(mlo) : 0,
+                                            mhi ? 32 + __builtin_ctz(mhi) : 32, mhi ? 64 - __builtin_clz(mhi) : 32);
         }
         wave_sync();
         float v[NF / 64];
@@ -2948,21 +2993,32 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
             const int o = lane + 64 * hh;                 // (R * WSZ + C) * NB + b
             const int b = o % NB, C = (o / NB) % WSZ, R = o / (NB * WSZ);
             const int col = R * NB + b;
-            unsigned long long m0 = s_mask[w][C + 1], m1 = s_mask[w][C];
             float s = 0.f;
-#ifdef SURF_DIAG_NORED
-            m0 = 0; m1 = 0; s = red[w][lane][col];
+            // cell column C: its own lanes at weight 1 - cfrac, then the lanes
+            // of column C - 1 at cfrac; ascending lanes, 4 reads in flight
+            auto run = [&](int lo, int hi, bool own) {
+                int k = lo;
+                for (; k + 4 <= hi; k += 4) {
+                    float r[4], c[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) { r[u] = red[w][k + u][col]; c[u] = s_cf[w][k + u]; }
+#pragma unroll
+                    for (int u = 0; u < 4; u++) s += r[u] * (own ? 1.f - c[u] : c[u]);
+                }
+                for (; k < hi; k++) {
+                    const float c = s_cf[w][k];
+                    s += red[w][k][col] * (own ? 1.f - c : c);
+                }
+            };
+#ifndef SURF_DIAG_NORED
+            const int4 q0 = s_run[w][C + 1], q1 = s_run[w][C];
+            run(q0.x, q0.y, true);
+            run(q0.z, q0.w, true);
+            run(q1.x, q1.y, false);
+            run(q1.z, q1.w, false);
+#else
+            s = red[w][lane][col];
 #endif
-            while (m0) {
-                const int jj = __builtin_ctzll(m0);
-                m0 &= m0 - 1;
-                s += red[w][jj][col] * (1.f - s_cf[w][jj]);
-            }
-            while (m1) {
-                const int jj = __builtin_ctzll(m1);
-                m1 &= m1 - 1;
-                s += red[w][jj][col] * s_cf[w][jj];
-            }
             v[hh] = s;
         }
         wave_sync();
@@ -2980,13 +3036,16 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
 
 hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
                            const int* counts, const int* offsets, const int* order, int nframes, float* desc,
-                           hipStream_t s)
+                           int* queue, hipStream_t s)
 {
     if (P.nfeat > 128) return hipErrorInvalidValue;
     const int grid = 2048;
     if (P.upright && P.wsz == 4) {
-        if (P.extend) k_describe_ur<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc);
-        else k_describe_ur<false><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc);
+        hipError_t e = hipMemsetAsync(queue, 0, kDescQueueBytes, s);
+        if (e != hipSuccess) return e;
+        if (P.extend)
+            k_describe_ur<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc, queue);
+        else k_describe_ur<false><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc, queue);
     } else if (P.upright) {
         k_describe<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, counts, offsets, order, nframes, desc);
     } else if (P.wsz == 4 && getenv("SURFHIP_ROT_ATOMIC") == nullptr) {
