@@ -445,7 +445,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     ALLOC(d->d_oct, sizeof(OctaveParams) * kMaxOct);
     ALLOC(d->ii, B * d->P.ii_stride * sizeof(int32_t));
     ALLOC(d->resp, B * d->tot_osize * sizeof(float));
-    ALLOC(d->colsum, B * d->nbands * d->CW * sizeof(uint32_t));
+    ALLOC(d->colsum, (size_t)integral_bands(d->H, B) * d->CW * sizeof(uint32_t));
     ALLOC(d->cand, B * d->cap * sizeof(surfhip_point));
     ALLOC(d->keys, B * d->cap * sizeof(uint32_t));
     ALLOC(d->cand_count, B * sizeof(int));

@@ -22,6 +22,16 @@ constexpr uint32_t kNoKey = 0xffffffffu;   // candidate slot of a rejected NMS s
 constexpr int kDescQ = 16;                  // describe work queues per XCD
 constexpr int kDescQueueBytes = 8 * kDescQ * 64 * 4;
 constexpr int kBandRows = 32;       // integral-image band height
+constexpr int kBandRowsSmall = 8;   // ... for batches of <= kSmallBatch frames
+constexpr int kSmallBatch = 8;
+// colsum entries (per column) the integral of a batch of up to max_batch frames needs
+inline long long integral_bands(int H, int max_batch)
+{
+    const long long big = (long long)max_batch * ((H + kBandRows - 1) / kBandRows);
+    const long long small = (long long)(max_batch < kSmallBatch ? max_batch : kSmallBatch) *
+                            ((H + kBandRowsSmall - 1) / kBandRowsSmall);
+    return big > small ? big : small;
+}
 constexpr int kScanRows = 16;       // NMS block rows per scan workgroup (4 per wave)
 constexpr int kItemCap = 64 * (kScanRows / 4);   // 2x2x2 blocks (= survivor slots) per scan item
 

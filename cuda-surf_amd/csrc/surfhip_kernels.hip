@@ -134,6 +134,18 @@ __device__ __forceinline__ void buf_st_nt(rsrc_t r, uint32_t off, float v)
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 2);
 }
 
+// compile-time loop: fn(std::integral_constant<int, K>) for K = 0 .. N-1
+template <typename Fn, int... Ks>
+__device__ __forceinline__ void static_for_seq(Fn&& fn, std::integer_sequence<int, Ks...>)
+{
+    (fn(std::integral_constant<int, Ks>{}), ...);
+}
+template <int N, typename Fn>
+__device__ __forceinline__ void static_for(Fn&& fn)
+{
+    static_for_seq(fn, std::make_integer_sequence<int, N>{});
+}
+
 // LDS ordering between the lanes of one wave, no wait: the LDS executes one
 // wave's DS instructions in issue order, so a ds_read issued after a
 // ds_write of the same wave sees it (and a later write cannot overtake an
@@ -185,22 +197,29 @@ __device__ __forceinline__ void load_px(const uint8_t* row, int x0, int W, uint3
 template <int CPT>
 __global__ __launch_bounds__(256) void k_ii_bandsum(const uint8_t* __restrict__ frames, int pitch,
                                                     long long fstride, int W, int H, int nbands,
-                                                    uint32_t* __restrict__ colsum, int CW)
+                                                    uint32_t* __restrict__ colsum, int CW, int br)
 {
     const int band = blockIdx.x, f = blockIdx.y;
     const int x0 = threadIdx.x * CPT;
     if (x0 >= W) return;
-    const int y0 = band * kBandRows;
-    const int rows = min(kBandRows, H - y0);
+    const int y0 = band * br;
+    const int rows = min(br, H - y0);
     const uint8_t* src = frames + (size_t)f * fstride + (size_t)y0 * pitch;
     uint32_t acc[CPT];
 #pragma unroll
     for (int k = 0; k < CPT; k++) acc[k] = 0u;
-    for (int r = 0; r < rows; r++) {
-        uint32_t px[CPT];
-        load_px<CPT>(src + (size_t)r * pitch, x0, W, px);
+    // 8 rows' loads in flight per iteration (rows past the band re-read the
+    // band's last row and are not added)
+    for (int r0 = 0; r0 < rows; r0 += 8) {
+        uint32_t px[8][CPT];
 #pragma unroll
-        for (int k = 0; k < CPT; k++) acc[k] += px[k];
+        for (int d = 0; d < 8; d++) load_px<CPT>(src + (size_t)min(r0 + d, rows - 1) * pitch, x0, W, px[d]);
+#pragma unroll
+        for (int d = 0; d < 8; d++)
+            if (r0 + d < rows) {
+#pragma unroll
+                for (int k = 0; k < CPT; k++) acc[k] += px[d][k];
+            }
     }
     uint32_t* dst = colsum + ((size_t)f * nbands + band) * CW + x0;
 #pragma unroll
@@ -214,10 +233,18 @@ __global__ __launch_bounds__(256) void k_ii_bandscan(uint32_t* __restrict__ cols
     if (x >= W) return;
     uint32_t* c = colsum + (size_t)f * nbands * CW + x;
     uint32_t run = 0u;
-    for (int b = 0; b < nbands; b++) {
-        const uint32_t v = c[(size_t)b * CW];
-        c[(size_t)b * CW] = run;
-        run += v;
+    // 16 bands' loads in flight per chunk (one memory latency per chunk,
+    // not per band)
+    for (int b0 = 0; b0 < nbands; b0 += 16) {
+        uint32_t v[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = (b0 + k < nbands) ? c[(size_t)(b0 + k) * CW] : 0u;
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            if (b0 + k < nbands) {
+                c[(size_t)(b0 + k) * CW] = run;
+                run += v[k];
+            }
     }
 }
 
@@ -254,14 +281,14 @@ template <int CPT>
 __global__ __launch_bounds__(256) void k_ii_fill(const uint8_t* __restrict__ frames, int pitch,
                                                  long long fstride, int W, int H, int nbands,
                                                  const uint32_t* __restrict__ colpre, int CW,
-                                                 int32_t* __restrict__ ii, int ip, long long istride)
+                                                 int32_t* __restrict__ ii, int ip, long long istride, int br)
 {
     __shared__ uint32_t lds4[4];
     const int band = blockIdx.x, f = blockIdx.y;
     const int x0 = threadIdx.x * CPT;
     const bool active = x0 <= W;               // thread owns integral columns x0..x0+CPT-1
-    const int y0 = band * kBandRows;
-    const int rows = min(kBandRows, H - y0);
+    const int y0 = band * br;
+    const int rows = min(br, H - y0);
     uint32_t acc[CPT];
     {
         const uint32_t* c = colpre + ((size_t)f * nbands + band) * CW;
@@ -303,16 +330,27 @@ __global__ __launch_bounds__(256) void k_ii_fill(const uint8_t* __restrict__ fra
 // Pass (C) with one wave per band and no barriers: lane l owns columns
 // 4 l + 256 t + j (t < NT, j < 4), so every load is 256 contiguous bytes and
 // every store 1 KiB; the row scan is NT wave scans with a running carry.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint32_t dpp_add(uint32_t v)
+{
+    return v + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWMASK, 0xf, false);
+}
+// inclusive scan over the wave's 64 lanes (gfx9 DPP: row shifts, then the
+// row_bcast:15 / row_bcast:31 carries) -- six VALU ops, no LDS round trip
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
+{
+    v = dpp_add<0x111, 0xf>(v);
+    v = dpp_add<0x112, 0xf>(v);
+    v = dpp_add<0x114, 0xf>(v);
+    v = dpp_add<0x118, 0xf>(v);
+    v = dpp_add<0x142, 0xa>(v);
+    v = dpp_add<0x143, 0xc>(v);
+    return v;
+}
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total)
 {
-    const unsigned lane = lane_id();
-    uint32_t inc = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t n = (uint32_t)__shfl_up((int)inc, d, 64);
-        if (lane >= (unsigned)d) inc += n;
-    }
-    total = (uint32_t)__shfl((int)inc, 63, 64);
+    const uint32_t inc = wave_incl_scan(v);
+    total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
     return inc - v;
 }
 
@@ -320,14 +358,15 @@ template <int NT>
 __global__ __launch_bounds__(256) void k_ii_fill_w(const uint8_t* __restrict__ frames, int pitch,
                                                    long long fstride, int W, int H, int nbands,
                                                    const uint32_t* __restrict__ colpre, int CW,
-                                                   int32_t* __restrict__ ii, int ip, long long istride, int nframes)
+                                                   int32_t* __restrict__ ii, int ip, long long istride, int nframes,
+                                                   int br)
 {
     const int gw = blockIdx.x * 4 + (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int f = gw / nbands, band = gw - f * nbands;
     if (f >= nframes) return;
     const int lane = (int)lane_id();
-    const int y0 = band * kBandRows;
-    const int rows = min(kBandRows, H - y0);
+    const int y0 = band * br;
+    const int rows = min(br, H - y0);
     // acc = ii[y0][x]: exclusive row scan of the column sums above the band
     uint32_t acc[NT][4];
     {
@@ -355,53 +394,72 @@ __global__ __launch_bounds__(256) void k_ii_fill_w(const uint8_t* __restrict__ f
         }
     }
     const uint8_t* src = frames + (size_t)f * fstride + (size_t)y0 * pitch;
-    for (int r = 0; r < rows; r++) {
-        const uint8_t* row = src + (size_t)r * pitch;
-        uint32_t wv[NT];
+    // the band's pixel rows stream through a ring of kFillAhead rows loaded
+    // ahead (the row scan no longer waits a memory latency per row: a single
+    // frame's 34 band waves were latency-bound)
+    constexpr int kFillAhead = 4;
+    uint32_t wq[kFillAhead][NT];
+    auto ldrow = [&](int r, uint32_t (&wv)[NT]) {
+        const uint8_t* row = src + (size_t)min(r, rows - 1) * pitch;     // past the band: a repeat, unused
 #pragma unroll
         for (int t = 0; t < NT; t++) {
             const int x = 4 * lane + 256 * t;
             wv[t] = (x + 4 <= pitch) ? *reinterpret_cast<const uint32_t*>(row + x) : 0u;
         }
-        uint32_t* dst = out + (size_t)(y0 + r + 1) * ip;
-        uint32_t carry = 0u;
+    };
+    static_for<kFillAhead>([&](auto dc) { ldrow(decltype(dc)::value, wq[decltype(dc)::value]); });
+    for (int r0 = 0; r0 < rows; r0 += kFillAhead) {
+        static_for<kFillAhead>([&](auto dc) {
+            constexpr int D = decltype(dc)::value;
+            const int r = r0 + D;
+            if (r >= rows) return;
+            uint32_t wv[NT];
 #pragma unroll
-        for (int t = 0; t < NT; t++) {
-            const int x = 4 * lane + 256 * t;
-            uint32_t p[4];
+            for (int t = 0; t < NT; t++) wv[t] = wq[D][t];
+            ldrow(r + kFillAhead, wq[D]);
+            uint32_t* dst = out + (size_t)(y0 + r + 1) * ip;
+            uint32_t carry = 0u;
 #pragma unroll
-            for (int j = 0; j < 4; j++) p[j] = (x + j < W) ? (wv[t] >> (8 * j)) & 0xffu : 0u;
-            const uint32_t e1 = p[0], e2 = e1 + p[1], e3 = e2 + p[2], tot = e3 + p[3];
-            uint32_t wt;
-            const uint32_t base = carry + wave_excl_scan(tot, wt);
-            carry += wt;
-            acc[t][0] += base; acc[t][1] += base + e1; acc[t][2] += base + e2; acc[t][3] += base + e3;
-            // pad columns (> W) stay zero: the flat reads of getTrace can land on them
-            if (x < ip)
-                *reinterpret_cast<uint4*>(dst + x) = make_uint4(x <= W ? acc[t][0] : 0u, x + 1 <= W ? acc[t][1] : 0u,
-                                                                x + 2 <= W ? acc[t][2] : 0u, x + 3 <= W ? acc[t][3] : 0u);
-        }
+            for (int t = 0; t < NT; t++) {
+                const int x = 4 * lane + 256 * t;
+                uint32_t p[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) p[j] = (x + j < W) ? (wv[t] >> (8 * j)) & 0xffu : 0u;
+                const uint32_t e1 = p[0], e2 = e1 + p[1], e3 = e2 + p[2], tot = e3 + p[3];
+                uint32_t wt;
+                const uint32_t base = carry + wave_excl_scan(tot, wt);
+                carry += wt;
+                acc[t][0] += base; acc[t][1] += base + e1; acc[t][2] += base + e2; acc[t][3] += base + e3;
+                // pad columns (> W) stay zero: the flat reads of getTrace can land on them
+                if (x < ip)
+                    *reinterpret_cast<uint4*>(dst + x) = make_uint4(x <= W ? acc[t][0] : 0u, x + 1 <= W ? acc[t][1] : 0u,
+                                                                    x + 2 <= W ? acc[t][2] : 0u, x + 3 <= W ? acc[t][3] : 0u);
+            }
+        });
     }
 }
 
 hipError_t launch_integral(const uint8_t* frames, int pitch, long long fstride, int nframes,
                            const FrameParams& P, uint32_t* colsum, int32_t* ii, hipStream_t s)
 {
-    const int nbands = (P.H + kBandRows - 1) / kBandRows;
+    // small batches: 8-row bands (4x the band waves of the fill pass, which
+    // is one wave per band) -- colsum is sized for both (integral_bands())
+    const int br = nframes <= kSmallBatch ? kBandRowsSmall : kBandRows;
+    const int nbands = (P.H + br - 1) / br;
     const int W = P.W;
     dim3 grid(nbands, nframes);
     if (W + 1 <= 2048) {
         const int CW = 2048;
-        k_ii_bandsum<8><<<grid, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW);
+        k_ii_bandsum<8><<<grid, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW, br);
         k_ii_bandscan<<<dim3((W + 255) / 256, nframes), 256, 0, s>>>(colsum, nbands, CW, W);
         k_ii_fill_w<8><<<(nbands * nframes + 3) / 4, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW,
-                                                                    ii, P.ip, P.ii_stride, nframes);
+                                                                    ii, P.ip, P.ii_stride, nframes, br);
     } else if (W + 1 <= 4096) {
         const int CW = 4096;
-        k_ii_bandsum<16><<<grid, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW);
+        k_ii_bandsum<16><<<grid, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW, br);
         k_ii_bandscan<<<dim3((W + 255) / 256, nframes), 256, 0, s>>>(colsum, nbands, CW, W);
         k_ii_fill_w<16><<<(nbands * nframes + 3) / 4, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum,
-                                                                     CW, ii, P.ip, P.ii_stride, nframes);
+                                                                     CW, ii, P.ip, P.ii_stride, nframes, br);
     } else {
         return hipErrorInvalidValue;
     }
@@ -1520,14 +1578,16 @@ __device__ __forceinline__ int wave_append(bool ok, int* counter)
 // appended to the frame's scan list with their canonical key (octave, level,
 // block row, block col) and argmax (s, r, c).
 // One workgroup = 4 waves x (64 block columns x kScanRows/4 block rows) of
-// one (frame, octave, level); XCD x takes frames x, x + 8, ...
+// one (frame, octave, level), a wave's rows in passes of 4 whose loads are
+// issued one pass ahead; XCD x takes frames x, x + 8, ...
 __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, const FrameParams& P,
                                               const OctaveParams* __restrict__ oct, const LaunchPlan& plan,
                                               uint32_t* __restrict__ scan_key, uint32_t* __restrict__ scan_src,
                                               int* __restrict__ item_count, int nitems_frame, int f, int gb, int wv,
                                               float* sbest, uint32_t* sinfo)
 {
-    constexpr int NU = kScanRows / 4;        // block rows per lane
+    constexpr int NU = 4;                    // block rows per lane per pass
+    constexpr int NIT = kScanRows / 4 / NU;  // passes: the next pass's loads are issued first
     const int o = octave_of(plan.nms_start, P.noct, gb);
     const OctaveParams& q = oct[o];
     const int nbx = plan.nms_nbx[o], nby = plan.nms_nby[o];
@@ -1535,57 +1595,10 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
     const int z = lb / (nbx * nby);
     lb -= z * nbx * nby;
     const int x = (lb % nbx) * 64 + (int)lane_id();
-    const int y0 = (lb / nbx) * kScanRows + wv;
+    const int ybase = (lb / nbx) * kScanRows + wv;     // this wave: rows ybase + 4 u, u < 4 NIT
     const OctView V = make_view(resp + (size_t)f * P.resp_stride, q, o);
     const int k = 2 * z + 1, mb = q.mb[z];
     const int j = mb + x * 2;
-    // ---- issue every row's 2x2x2 block loads first (memory-level parallelism)
-    float v[NU][8];
-    bool in[NU];
-#pragma unroll
-    for (int u = 0; u < NU; u++) {
-        const int y = y0 + 4 * u, i = mb + y * 2;
-        in[u] = x < q.nms_gx && y < q.nms_gy && i < q.sh - mb && j < q.sw - mb;
-        const int ii = in[u] ? i : mb, jj = in[u] ? j : mb;
-        V.pair(k, ii, jj, v[u][0], v[u][1]);
-        V.pair(k, ii + 1, jj, v[u][2], v[u][3]);
-        V.pair(k + 1, ii, jj, v[u][4], v[u][5]);
-        V.pair(k + 1, ii + 1, jj, v[u][6], v[u][7]);
-    }
-    // ---- argmax over the 2x2x2 block in the reference's order (k: w,x,y,z;
-    // k+1: w,x,y,z), strict '>', threshold and top-scale rejection
-    // (surfd.cu:678-756)
-    bool cnd[NU];
-    float bst[NU];
-    int cs[NU];
-#pragma unroll
-    for (int u = 0; u < NU; u++) {
-        int cas = 0;
-        float best = v[u][0];
-#pragma unroll
-        for (int t = 1; t < 8; t++)
-            if (v[u][t] > best) { best = v[u][t]; cas = t; }
-        cnd[u] = in[u] && !(best < P.thresh * 0.8f || (k + 1 == P.max_scale - 1 && cas > 3));
-        bst[u] = best;
-        cs[u] = cas;
-    }
-    // ---- compact the candidates of all NU rows into dense lanes (LDS), so
-    // the 19-neighbour test costs 19 loads per 64 candidates, not per row
-    unsigned long long m[NU];
-    int ncand = 0;
-#pragma unroll
-    for (int u = 0; u < NU; u++) {
-        m[u] = __ballot(cnd[u]);
-        if (cnd[u]) {
-            const int slot = ncand + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m[u] >> 32),
-                                                                   __builtin_amdgcn_mbcnt_lo((unsigned)m[u], 0u));
-            sbest[slot] = bst[u];
-            sinfo[slot] = ((uint32_t)u << 9) | ((uint32_t)cs[u] << 6) | lane_id();
-        }
-        ncand += (int)__popcll(m[u]);
-    }
-    if (ncand == 0) return;
-    wave_sync();
     const int bx0 = (lb % nbx) * 64;
     // survivors go to this wave item's own region (no atomics): kItemCap
     // entries at item * kItemCap, the count in item_count[item]
@@ -1593,45 +1606,102 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
     uint32_t* rkey = scan_key + item * kItemCap;
     uint32_t* rsrc_ = scan_src + item * kItemCap;
     int nsurv = 0;
-    for (int c0 = 0; c0 < ncand; c0 += 64) {
-        const int ci = c0 + (int)lane_id();
-        bool ok = false;
-        int s = 0, r = 0, c = 0, x = 0, y = 0;
-        if (ci < ncand) {
-            const float best = sbest[ci];
-            const uint32_t info = sinfo[ci];
-            const int u = (int)(info >> 9), cas = (int)((info >> 6) & 7u);
-            x = bx0 + (int)(info & 63u);
-            y = y0 + 4 * u;
-            const int i = mb + y * 2, j = mb + x * 2;
-            s = k + (cas >> 2); r = i + ((cas >> 1) & 1); c = j + (cas & 1);
-            const int ds = (cas >> 2) ? 1 : -1, dr = ((cas >> 1) & 1) ? 1 : -1, dc = (cas & 1) ? 1 : -1;
-            const int so = s + ds, si = s - ds;
-            const int rn = r + dr, rp = r - dr, cn = c + dc;
-            // the 19 neighbours outside the block, ties survive (surfd.cu:757-792);
-            // all loads issued before any compare
-            const float nb[19] = {V(so, rp, c - 1), V(so, rp, c), V(so, rp, c + 1),
-                                  V(so, r, c - 1),  V(so, r, c),  V(so, r, c + 1),
-                                  V(so, rn, c - 1), V(so, rn, c), V(so, rn, c + 1),
-                                  V(s, rn, c - 1),  V(s, rn, c),  V(s, rn, c + 1),
-                                  V(s, r, cn),      V(s, rp, cn),
-                                  V(si, rn, c - 1), V(si, rn, c), V(si, rn, c + 1),
-                                  V(si, rp, cn),    V(si, r, cn)};
-            ok = true;
+    // ---- a pass's 2x2x2 block loads, all issued before any use
+    float v[2][NU][8];
+    bool in[2][NU];
+    auto load = [&](int it, float (&vv)[NU][8], bool (&inn)[NU]) {
 #pragma unroll
-            for (int t = 0; t < 19; t++) ok = ok && !(best < nb[t]);
+        for (int u = 0; u < NU; u++) {
+            const int y = ybase + 4 * (it * NU + u), i = mb + y * 2;
+            inn[u] = x < q.nms_gx && y < q.nms_gy && i < q.sh - mb && j < q.sw - mb;
+            const int ii = inn[u] ? i : mb, jj = inn[u] ? j : mb;
+            V.pair(k, ii, jj, vv[u][0], vv[u][1]);
+            V.pair(k, ii + 1, jj, vv[u][2], vv[u][3]);
+            V.pair(k + 1, ii, jj, vv[u][4], vv[u][5]);
+            V.pair(k + 1, ii + 1, jj, vv[u][6], vv[u][7]);
         }
-        const unsigned long long mo = __ballot(ok);
-        if (ok) {
-            const int slot = nsurv + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mo >> 32),
-                                                                   __builtin_amdgcn_mbcnt_lo((unsigned)mo, 0u));
-            rkey[slot] = ((uint32_t)o << 29) | ((uint32_t)z << 28) | ((uint32_t)y << 14) | (uint32_t)x;
-            rsrc_[slot] = ((uint32_t)s << 28) | ((uint32_t)r << 14) | (uint32_t)c;
+    };
+    load(0, v[0], in[0]);
+    static_for<NIT>([&](auto itc) {
+        constexpr int it = decltype(itc)::value;
+        if constexpr (it + 1 < NIT) load(it + 1, v[(it + 1) & 1], in[(it + 1) & 1]);
+        const float (&vc)[NU][8] = v[it & 1];
+        const bool (&ic)[NU] = in[it & 1];
+        const int y0 = ybase + 4 * it * NU;
+        // ---- argmax over the 2x2x2 block in the reference's order (k: w,x,y,z;
+        // k+1: w,x,y,z), strict '>', threshold and top-scale rejection
+        // (surfd.cu:678-756)
+        bool cnd[NU];
+        float bst[NU];
+        int cs[NU];
+#pragma unroll
+        for (int u = 0; u < NU; u++) {
+            int cas = 0;
+            float best = vc[u][0];
+#pragma unroll
+            for (int t = 1; t < 8; t++)
+                if (vc[u][t] > best) { best = vc[u][t]; cas = t; }
+            cnd[u] = ic[u] && !(best < P.thresh * 0.8f || (k + 1 == P.max_scale - 1 && cas > 3));
+            bst[u] = best;
+            cs[u] = cas;
         }
-        nsurv += (int)__popcll(mo);
-    }
+        // ---- compact the candidates of the pass's NU rows into dense lanes
+        // (LDS), so the 19-neighbour test costs 19 loads per 64 candidates
+        unsigned long long m[NU];
+        int ncand = 0;
+#pragma unroll
+        for (int u = 0; u < NU; u++) {
+            m[u] = __ballot(cnd[u]);
+            if (cnd[u]) {
+                const int slot = ncand + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m[u] >> 32),
+                                                                       __builtin_amdgcn_mbcnt_lo((unsigned)m[u], 0u));
+                sbest[slot] = bst[u];
+                sinfo[slot] = ((uint32_t)u << 9) | ((uint32_t)cs[u] << 6) | lane_id();
+            }
+            ncand += (int)__popcll(m[u]);
+        }
+        if (ncand == 0) return;
+        wave_sync();
+        for (int c0 = 0; c0 < ncand; c0 += 64) {
+            const int ci = c0 + (int)lane_id();
+            bool ok = false;
+            int s = 0, r = 0, c = 0, xx = 0, y = 0;
+            if (ci < ncand) {
+                const float best = sbest[ci];
+                const uint32_t info = sinfo[ci];
+                const int u = (int)(info >> 9), cas = (int)((info >> 6) & 7u);
+                xx = bx0 + (int)(info & 63u);
+                y = y0 + 4 * u;
+                const int i = mb + y * 2, jx = mb + xx * 2;
+                s = k + (cas >> 2); r = i + ((cas >> 1) & 1); c = jx + (cas & 1);
+                const int ds = (cas >> 2) ? 1 : -1, dr = ((cas >> 1) & 1) ? 1 : -1, dc = (cas & 1) ? 1 : -1;
+                const int so = s + ds, si = s - ds;
+                const int rn = r + dr, rp = r - dr, cn = c + dc;
+                // the 19 neighbours outside the block, ties survive (surfd.cu:757-792);
+                // all loads issued before any compare
+                const float nb[19] = {V(so, rp, c - 1), V(so, rp, c), V(so, rp, c + 1),
+                                      V(so, r, c - 1),  V(so, r, c),  V(so, r, c + 1),
+                                      V(so, rn, c - 1), V(so, rn, c), V(so, rn, c + 1),
+                                      V(s, rn, c - 1),  V(s, rn, c),  V(s, rn, c + 1),
+                                      V(s, r, cn),      V(s, rp, cn),
+                                      V(si, rn, c - 1), V(si, rn, c), V(si, rn, c + 1),
+                                      V(si, rp, cn),    V(si, r, cn)};
+                ok = true;
+#pragma unroll
+                for (int t = 0; t < 19; t++) ok = ok && !(best < nb[t]);
+            }
+            const unsigned long long mo = __ballot(ok);
+            if (ok) {
+                const int slot = nsurv + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mo >> 32),
+                                                                       __builtin_amdgcn_mbcnt_lo((unsigned)mo, 0u));
+                rkey[slot] = ((uint32_t)o << 29) | ((uint32_t)z << 28) | ((uint32_t)y << 14) | (uint32_t)xx;
+                rsrc_[slot] = ((uint32_t)s << 28) | ((uint32_t)r << 14) | (uint32_t)c;
+            }
+            nsurv += (int)__popcll(mo);
+        }
+        wave_sync();                          // sbest / sinfo are rewritten by the next pass
+    });
     if (lane_id() == 0u && nsurv > 0) item_count[item] = nsurv;
-    wave_sync();
 }
 
 __global__ __launch_bounds__(256) void k_nms_scan(const float* __restrict__ resp, FrameParams P,
@@ -1639,8 +1709,8 @@ __global__ __launch_bounds__(256) void k_nms_scan(const float* __restrict__ resp
                                                   uint32_t* __restrict__ scan_key, uint32_t* __restrict__ scan_src,
                                                   int* __restrict__ item_count, int nframes)
 {
-    __shared__ float sbest[4][64 * (kScanRows / 4)];
-    __shared__ uint32_t sinfo[4][64 * (kScanRows / 4)];
+    __shared__ float sbest[4][64 * 4];                // one pass's candidates per wave
+    __shared__ uint32_t sinfo[4][64 * 4];
     int f, gb;
     if (!xcd_frame_block(plan.nms_start[kMaxOct], nframes, f, gb)) return;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1874,6 +1944,73 @@ __global__ __launch_bounds__(1024) void k_sort(const surfhip_point* __restrict__
     for (int t = threadIdx.x; t < keep; t += blockDim.x) ord[t] = (int)(bk[t] & 0xfffffu);
 }
 
+// Small batches (nframes <= kRankBatch): the canonical order by ranks,
+// spread over many workgroups per frame instead of one bitonic workgroup
+// (config #2: one frame's sort ran on one CU of 256).  Valid keys are unique
+// (one survivor per 2x2x2 block), so a valid candidate's rank is the number
+// of keys below its own -- exactly its position in the bitonic result;
+// rejected slots (kNoKey) sort last and are dropped.  Workgroup r of a frame
+// ranks candidates [256 r, 256 r + 256) against all of the frame's keys
+// (staged in LDS when they fit).  Processing order for describe = canonical.
+constexpr int kRankBatch = 8;
+constexpr int kRankLds = 16384;
+__global__ __launch_bounds__(256) void k_sort_rank(const surfhip_point* __restrict__ cand,
+                                                   const uint32_t* __restrict__ keys,
+                                                   const int* __restrict__ cand_count,
+                                                   const int* __restrict__ soff, int items_per_frame, int cap,
+                                                   int wgs_per_frame, surfhip_point* __restrict__ out, int max_pts,
+                                                   int* __restrict__ out_count, int* __restrict__ order,
+                                                   int* __restrict__ status)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t sk[kRankLds];
+    __shared__ int nvalid;
+    const int f = blockIdx.x / wgs_per_frame, r = blockIdx.x - f * wgs_per_frame;
+    const int cnt = min(soff[(f + 1) * items_per_frame] - soff[f * items_per_frame], cap);
+    const uint32_t* fk = keys + (size_t)f * cap;
+    if (r > 0 && r * 256 >= cnt) return;      // nothing to rank here (workgroup 0 writes the count)
+    if (threadIdx.x == 0) nvalid = 0;
+    __syncthreads();
+    const bool lds = cnt <= kRankLds;
+    int mine = 0;
+    if (lds) {
+        for (int i = threadIdx.x; i < cnt; i += 256) {
+            const uint32_t k = fk[i];
+            sk[i] = k;
+            mine += k != kNoKey;
+        }
+    } else {
+        for (int i = threadIdx.x; i < cnt; i += 256) mine += fk[i] != kNoKey;
+    }
+    if (mine) atomicAdd(&nvalid, mine);
+    __syncthreads();
+    const int valid = nvalid;
+    const int keep = min(valid, max_pts);
+    if (r == 0 && threadIdx.x == 0) {
+        out_count[f] = keep;
+        if (cand_count[f] > valid) atomicOr(status, 1);
+    }
+    const int i = r * 256 + (int)threadIdx.x;
+    if (i >= cnt) return;
+    const uint32_t ki = lds ? sk[i] : fk[i];
+    if (ki == kNoKey) return;
+    int rank = 0;
+    if (lds) {
+        const uint4* s4 = reinterpret_cast<const uint4*>(sk);
+        const int n4 = cnt >> 2;
+        for (int j = 0; j < n4; j++) {
+            const uint4 q = s4[j];                          // broadcast read
+            rank += (q.x < ki) + (q.y < ki) + (q.z < ki) + (q.w < ki);
+        }
+        for (int j = n4 * 4; j < cnt; j++) rank += sk[j] < ki;
+    } else {
+        for (int j = 0; j < cnt; j++) rank += fk[j] < ki;
+    }
+    if (rank < keep) {
+        out[(size_t)f * max_pts + rank] = cand[(size_t)f * cap + i];
+        order[(size_t)f * max_pts + rank] = rank;
+    }
+}
+
 __global__ __launch_bounds__(1024) void k_offsets(const int* __restrict__ counts, int nframes, int* __restrict__ offsets)
 {
     __shared__ int part[1024];
@@ -1899,11 +2036,17 @@ hipError_t launch_sort(const surfhip_point* cand, const uint32_t* keys, uint64_t
                        surfhip_point* out, int max_pts, int* out_count, int* offsets, int* order, int* status,
                        hipStream_t s)
 {
-    hipError_t e = set_max_lds(reinterpret_cast<const void*>(&k_sort), (int)(kSortCap * sizeof(uint64_t)));
-    if (e != hipSuccess) return e;
-    k_sort<<<nframes, 1024, kSortCap * sizeof(uint64_t), s>>>(cand, keys, gscratch, cand_count, soff,
-                                                              items_per_frame, cap, out, max_pts, out_count, order,
-                                                              status);
+    if (nframes <= kRankBatch && getenv("SURFHIP_SORT_BITONIC") == nullptr) {
+        const int per = (cap + 255) / 256;
+        k_sort_rank<<<nframes * per, 256, 0, s>>>(cand, keys, cand_count, soff, items_per_frame, cap, per, out,
+                                                  max_pts, out_count, order, status);
+    } else {
+        hipError_t e = set_max_lds(reinterpret_cast<const void*>(&k_sort), (int)(kSortCap * sizeof(uint64_t)));
+        if (e != hipSuccess) return e;
+        k_sort<<<nframes, 1024, kSortCap * sizeof(uint64_t), s>>>(cand, keys, gscratch, cand_count, soff,
+                                                                  items_per_frame, cap, out, max_pts, out_count,
+                                                                  order, status);
+    }
     k_offsets<<<1, 1024, 0, s>>>(out_count, nframes, offsets);
     return hipGetLastError();
 }
