@@ -2490,8 +2490,16 @@ __global__ __launch_bounds__(256) void k_describe_rot(const int32_t* __restrict_
         const surfhip_point p = *pp;
         const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
         const int ip = P.ip;
+#ifdef SURF_DIAG_NOORI
+        const float ori = 0.3f;
+#else
         const float ori = orientation_wave(I, P, p, S.ori, lane);
+#endif
         if (lane == 0) pp->ori = ori;
+#ifdef SURF_DIAG_NODESC
+        if (lane < 2) desc[((size_t)f * max_pts + i) * NF + lane] = ori;
+        continue;
+#endif
 
         const DescAt at = desc_at(P.doubled, p);
         const float scale = at.scale;
@@ -2570,6 +2578,9 @@ __global__ __launch_bounds__(256) void k_describe_rot(const int32_t* __restrict_
             }
             const int cj = sj++;
             const float fi = (float)si, fj = (float)cj;
+            // IEEE division as the reference: rpos^2 + cpos^2 indexes the
+            // Gaussian LUT, so one ulp can move a sample to the next weight
+            // (x * (1 / spacing) broke config #5 parity at 1.3e-3 L2)
             const float rpos = ((fstep * ((cose * fi) + (sine * fj))) - fracr) / spacing;
             const float cpos = ((fstep * (((-sine) * fi) + (cose * fj))) - fracc) / spacing;
             const float rx = rpos + wofs, cx = cpos + wofs;
