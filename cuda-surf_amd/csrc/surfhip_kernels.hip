@@ -1416,25 +1416,23 @@ struct OctView {
     const float* F;                 // the frame's response block
     int cur, prev;                  // float offsets of this octave's / the previous octave's plane 0 (-1: none)
     int sp, osize, psp, posize;
+    // branch-free (selects): a branch around a load makes hipcc wait for the
+    // loads issued before it at the join, which serialised the NMS scan's 32
+    // block loads into 16 memory round trips
     __device__ __forceinline__ int off(int s, int r, int c) const
     {
-        if (prev >= 0 && s < 2) return prev + (s == 0 ? 2 : 4) * posize + (2 * r) * psp + 2 * c;
-        return cur + s * osize + r * sp + c;
+        const bool h = prev >= 0 && s < 2;          // planes 0/1 of octave > 0: previous octave, 2x stride
+        const int base = h ? prev + (s == 0 ? 2 : 4) * posize : cur + s * osize;
+        return base + r * (h ? 2 * psp : sp) + (h ? 2 * c : c);
     }
     __device__ __forceinline__ float operator()(int s, int r, int c) const { return F[off(s, r, c)]; }
-    // (s, r, c) and (s, r, c + 1): one 8-byte load on a materialised plane
-    // (dword alignment is enough for global_load_dwordx2)
+    // (s, r, c) and (s, r, c + 1)
     __device__ __forceinline__ void pair(int s, int r, int c, float& a, float& b) const
     {
-        struct __attribute__((packed, aligned(4))) F2 { float x, y; };
-        if (prev >= 0 && s < 2) {
-            a = F[off(s, r, c)];
-            b = F[off(s, r, c + 1)];
-        } else {
-            const F2 v = *reinterpret_cast<const F2*>(F + off(s, r, c));
-            a = v.x;
-            b = v.y;
-        }
+        const bool h = prev >= 0 && s < 2;
+        const int o = off(s, r, c);
+        a = F[o];
+        b = F[o + (h ? 2 : 1)];
     }
 };
 
