@@ -82,7 +82,7 @@ struct LaunchPlan {
     int o0_lds;                     // octave 0 on the LDS-tiled kernel (k_hess_o0)
     int o0_nbx, o0_blocks;
     int o0_v, o0_vstrips;           // octave 0 on the u8 vertical-streaming kernel (k_hess_v0)
-    int o0_split;                   // k_hess_v0 scale groups: 0 one launch, 1 {0-2}{3-4}, 2 {0-1}{2-3}{4}
+    int o0_split;                   // octave-0 kernel variant (make_plan; 44 = k_hess_q0 default, 0 = k_hess_v0)
     int o1_lds;                     // octave 1 on the LDS ring (k_hess_o1)
     int o1_v, o1_vstrips;           // octave 1 on the u8 vertical-streaming kernel (k_hess_v1)
     int vfar_n;                     // octaves 2 .. 1 + vfar_n on k_hess_vfar (u8 vertical streaming)

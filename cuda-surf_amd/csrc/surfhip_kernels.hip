@@ -710,6 +710,8 @@ __global__ __launch_bounds__(o0::THREADS, 4) void k_hess_o0(const int32_t* __res
 #include "surfhip_hess_vfar.inc"
 #include "surfhip_hess_s0.inc"
 #include "surfhip_hess_f0.inc"
+#include "surfhip_hess_p0.inc"
+#include "surfhip_hess_q0.inc"
 
 // ----------------------------------------------------------------------
 // Octave 1 (4 px between samples, lobes 15/19/23: corner offsets -34..35):
@@ -982,7 +984,9 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
     plan.o0_nbx = (oct[0].sw + o0::TXS - 1) / o0::TXS;     // strips per frame
     plan.o0_blocks = plan.o0_nbx;
     plan.o0_v = plan.o0_lds && getenv("SURFHIP_O0_RING") == nullptr;   // A/B switch back to k_hess_o0
-    plan.o0_split = getenv("SURFHIP_V0_SPLIT") ? atoi(getenv("SURFHIP_V0_SPLIT")) : 0;   // k_hess_v0 scale groups
+    // octave-0 kernel: default k_hess_q0<4, 1, 2> (packed fp32 box sums); SURFHIP_V0_SPLIT
+    // selects the A/B variants (0 = k_hess_v0, 1/2 its scale splits, 20/21, 30-32, 40-46)
+    plan.o0_split = getenv("SURFHIP_V0_SPLIT") ? atoi(getenv("SURFHIP_V0_SPLIT")) : 44;
     plan.o0_vstrips = (oct[0].sw + 63) / 64;
     plan.o1_lds = !gather && P.noct > 1 && o1_lds_ok(P, oct[1]);
     plan.o1_v = plan.o1_lds && getenv("SURFHIP_O1_RING") == nullptr;   // A/B switch back to k_hess_o1
@@ -1317,6 +1321,20 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
             const int segr = (q.sh + 2 * npairs - 1) / (2 * npairs);
             const int nb = (nframes >= 8 ? nf8 : nframes) * ns * npairs;
             k_hess_f0<<<dim3(nb), f0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, q, ns, npairs, segr, nframes);
+        } else if (split == 30 || split == 31 || split == 32) {   // software-pipelined, branch-free
+            const dim3 gp(8 * ((per_xcd + p0::WAVES - 1) / p0::WAVES));
+            if (split == 30)
+                k_hess_p0<4, 1, false><<<gp, p0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0], plan.o0_vstrips, nframes);
+            else if (split == 31)
+                k_hess_p0<4, 1, true><<<gp, p0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0], plan.o0_vstrips, nframes);
+            else
+                k_hess_p0<6, 1, true><<<gp, p0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0], plan.o0_vstrips, nframes);
+        } else if (split >= 40 && split <= 49) {   // packed fp32 box sums, rebased local integral
+            const dim3 gq(8 * ((per_xcd + q0::WAVES - 1) / q0::WAVES));
+            auto* kq = split == 40 ? &k_hess_q0<2, 1, 1> : split == 41 ? &k_hess_q0<2, 1, 2> : split == 42 ? &k_hess_q0<2, 1, 3>
+                     : split == 43 ? &k_hess_q0<3, 1, 2> : split == 44 ? &k_hess_q0<4, 1, 2> : split == 45 ? &k_hess_q0<4, 1, 3>
+                     : &k_hess_q0<3, 1, 3>;
+            kq<<<gq, q0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0], plan.o0_vstrips, nframes);
         } else if (split == 10) {   // experiments
             k_hess_v0<4, 0, 0x1f><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
                                                             plan.o0_vstrips, nframes);

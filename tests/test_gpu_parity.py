@@ -120,8 +120,46 @@ def test_hessian_planes_bit_exact(surf, orc, w, h, noct):
         assert same.all(), f"octave {o} scale {s}: {(~same).sum()} cells differ, first at {np.argwhere(~same)[0]}"
 
 
-@pytest.mark.parametrize("env", ["SURFHIP_O0_RING", "SURFHIP_O1_RING", "SURFHIP_FAR_V", "SURFHIP_V0_SPLIT=1",
-                                 "SURFHIP_V0_SPLIT=2", "SURFHIP_V0_SPLIT=20", "SURFHIP_V0_SPLIT=21", "SURFHIP_HESS_GATHER=1"])
+def _extreme_frame(kind, w, h, pitch):
+    """Frames that drive the box sums to their extremes: every value the
+    Hessian kernels hold must stay an exact integer (k_hess_q0 keeps them in
+    fp32 below 2^24 by rebasing its local integral)."""
+    rng = np.random.default_rng(5)
+    f = np.zeros((h, pitch), np.uint8)
+    if kind == "white":
+        f[:, :w] = 255
+    elif kind == "noise":
+        f[:, :w] = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    elif kind == "vstripes":       # 0/255 columns of period 6: large dxx, zero dyy
+        f[:, :w] = np.where((np.arange(w) // 3) % 2 == 0, 255, 0).astype(np.uint8)[None, :]
+    elif kind == "checker":        # 7x5 blocks: large dxy
+        yy, xx = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+        f[:, :w] = np.where(((yy // 5) + (xx // 7)) % 2 == 0, 255, 0).astype(np.uint8)
+    return f
+
+
+@pytest.mark.parametrize("kind", ["white", "noise", "vstripes", "checker"])
+@pytest.mark.parametrize("env", ["SURFHIP_V0_SPLIT=44", "SURFHIP_V0_SPLIT=0"])
+def test_hessian_planes_extreme_frames(surf, orc, monkeypatch, kind, env):
+    w, h = 1920, 1080
+    name, _, val = env.partition("=")
+    monkeypatch.setenv(name, val)
+    frames = _extreme_frame(kind, w, h, surf.align_up(w, 128))[None]
+    param = surf.make_param(4, 4.0, upright=True)
+    res = gpu_run(surf, param, frames, w, h, want_ws=True, desc=False)
+    op = orc.make_param(4, 4.0, upright=True)
+    _, ref, g, octs = orc.hessian(op, frames[0], w, h)
+    got = res["resp"][0]
+    for (o, s, rp), (_, _, gp) in zip(_plane_views(ref, g, octs, op), _plane_views(got, g, octs, op)):
+        same = rp.view(np.uint32) == gp.view(np.uint32)
+        assert same.all(), f"{kind}/{env}: octave {o} scale {s}: {(~same).sum()} cells differ"
+
+
+@pytest.mark.parametrize("env", ["SURFHIP_O0_RING", "SURFHIP_O1_RING", "SURFHIP_FAR_V", "SURFHIP_V0_SPLIT=0", "SURFHIP_V0_SPLIT=1",
+                                 "SURFHIP_V0_SPLIT=2", "SURFHIP_V0_SPLIT=20", "SURFHIP_V0_SPLIT=21", "SURFHIP_V0_SPLIT=30",
+                                 "SURFHIP_V0_SPLIT=31", "SURFHIP_V0_SPLIT=32", "SURFHIP_V0_SPLIT=40",
+                                 "SURFHIP_V0_SPLIT=41", "SURFHIP_V0_SPLIT=42", "SURFHIP_V0_SPLIT=43",
+                                 "SURFHIP_V0_SPLIT=44", "SURFHIP_V0_SPLIT=45", "SURFHIP_V0_SPLIT=46", "SURFHIP_HESS_GATHER=1"])
 @pytest.mark.parametrize("w,h,noct", [(640, 480, 4), (1920, 1080, 4)])
 def test_hessian_alternate_kernels_bit_exact(surf, orc, monkeypatch, env, w, h, noct):
     """The selectable Hessian kernels (integral-image rings for octaves 0/1,
