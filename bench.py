@@ -351,8 +351,7 @@ def main():
             "keypoints_per_frame": round(kp_total_batch / (world * B), 1),
             "keypoints_per_step": kp_total_batch,
             "stage_ms_per_step_serial": {k: round(v / nprof, 4) for k, v in stage_acc.items()},
-            "roofline": {"kernel": "Hessian stage, all octaves in series: k_hess_v0 (octave 0) + k_hess_v1 "
-                                   "(octave 1) + k_hess_far (octaves >= 2), per batch",
+            "roofline": {"kernel": "Hessian stage, all octaves in series: " + det.hessian_kernels() + ", per batch",
                          "bound": "hbm",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -115,6 +115,7 @@ _sigs = {
     "surfhip_run_integral": (_i, [_vp, _vp, _i, _i, _sz]),
     "surfhip_run_hessian": (_i, [_vp, _i]),
     "surfhip_hessian_bytes_per_frame": (C.c_longlong, [_vp]),
+    "surfhip_hessian_plan": (C.c_int, [_vp, C.c_char_p, C.c_int]),
     "surfhip_slab_bytes": (_sz, [_i, _i, _i]),
     "surfhip_batch_total": (_i, [_vp, _i, C.POINTER(_i)]),
     "surfhip_pack_slab": (_i, [_vp, _vp, _vp, _vp, _i, _vp]),
@@ -319,6 +320,14 @@ class Detector:
 
     def hessian_bytes_per_frame(self) -> int:
         return int(_lib.surfhip_hessian_bytes_per_frame(self.h))
+
+    def hessian_kernels(self) -> str:
+        """The Hessian stage's kernels of this detector's plan (surfhip_hessian_plan)."""
+        buf = C.create_string_buffer(256)
+        n = _lib.surfhip_hessian_plan(self.h, buf, len(buf))
+        if n < 0:
+            check(n, "hessian_plan")
+        return buf.value.decode()
 
     def slab_bytes(self, nframes: int, total: int, desc: bool = True) -> int:
         return int(_lib.surfhip_slab_bytes(nframes, total, self.nfeatures if desc else 0))

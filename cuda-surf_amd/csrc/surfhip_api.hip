@@ -710,6 +710,18 @@ int surfhip_detector_geometry(surfhip_detector* d, int* iwhp, int* swhp, long lo
 
 long long surfhip_hessian_bytes_per_frame(surfhip_detector* d) { return d ? d->hess_bytes : -1; }
 
+int surfhip_hessian_plan(surfhip_detector* d, char* buf, int len)
+{
+    if (!d) return SURFHIP_ERR_INVALID;
+    const std::string t = hessian_plan_text(d->plan, d->far, d->P);
+    if (buf && len > 0) {
+        const size_t n = std::min((size_t)len - 1, t.size());
+        memcpy(buf, t.data(), n);
+        buf[n] = 0;
+    }
+    return (int)t.size();
+}
+
 size_t surfhip_slab_bytes(int nframes, int total, int nfeatures)
 {
     return 16 + (((size_t)nframes * 4 + 15) & ~(size_t)15) +

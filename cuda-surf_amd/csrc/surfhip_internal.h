@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "surfhip.h"
 
 namespace surfhip {
@@ -85,6 +87,7 @@ struct LaunchPlan {
     int o0_split;                   // octave-0 kernel variant (make_plan; 44 = k_hess_q0 default, 0 = k_hess_v0)
     int o1_lds;                     // octave 1 on the LDS ring (k_hess_o1)
     int o1_v, o1_vstrips;           // octave 1 on the u8 vertical-streaming kernel (k_hess_v1)
+    int o1_q;                       // ... its packed-fp32 variant (k_hess_q1)
     int vfar_n;                     // octaves 2 .. 1 + vfar_n on k_hess_vfar (u8 vertical streaming)
     int o1_nbx;
 };
@@ -93,7 +96,10 @@ struct LaunchPlan {
 // corner row (dr) and bucketed by dr mod delta; see surfhip_kernels.hip.
 namespace farc {
 constexpr int MAXO = 3;             // far octaves on the kernel (2, 3, 4)
-constexpr int STRIP = 256;          // image columns per workgroup strip
+#ifndef SURF_FAR_STRIP
+#define SURF_FAR_STRIP 256
+#endif
+constexpr int STRIP = SURF_FAR_STRIP; // image columns per workgroup strip
 constexpr int R = 8;                // image rows per step (one wave each)
 constexpr int THREADS = 64 * R;
 constexpr int NA = 32;              // accumulator rows (sample rows in flight, a power of 2)
@@ -113,6 +119,8 @@ struct FarPlan {
 // at 8 frames, 12,474 vs 14,085 at 16).
 constexpr int kGatherBatch = 8;
 void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, FarPlan& far, int max_batch);
+// the Hessian stage's kernels of a plan, as text (surfhip_hessian_plan)
+std::string hessian_plan_text(const LaunchPlan& plan, const FarPlan& far, const FrameParams& P);
 
 // frames may be null (no u8 source known): every octave then reads the integral image
 hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, const int32_t* ii, float* resp,

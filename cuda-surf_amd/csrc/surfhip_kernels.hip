@@ -708,10 +708,8 @@ __global__ __launch_bounds__(o0::THREADS, 4) void k_hess_o0(const int32_t* __res
 #include "surfhip_hess_v0.inc"
 #include "surfhip_hess_v1.inc"
 #include "surfhip_hess_vfar.inc"
-#include "surfhip_hess_s0.inc"
-#include "surfhip_hess_f0.inc"
-#include "surfhip_hess_p0.inc"
 #include "surfhip_hess_q0.inc"
+#include "surfhip_hess_q1.inc"
 
 // ----------------------------------------------------------------------
 // Octave 1 (4 px between samples, lobes 15/19/23: corner offsets -34..35):
@@ -984,12 +982,14 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
     plan.o0_nbx = (oct[0].sw + o0::TXS - 1) / o0::TXS;     // strips per frame
     plan.o0_blocks = plan.o0_nbx;
     plan.o0_v = plan.o0_lds && getenv("SURFHIP_O0_RING") == nullptr;   // A/B switch back to k_hess_o0
-    // octave-0 kernel: default k_hess_q0<4, 1, 2> (packed fp32 box sums); SURFHIP_V0_SPLIT
-    // selects the A/B variants (0 = k_hess_v0, 1/2 its scale splits, 20/21, 30-32, 40-46)
+    // octave-0 kernel: default k_hess_q0<4, 1, 2> (packed fp32 box sums); SURFHIP_V0_SPLIT=0
+    // selects k_hess_v0 (integer accumulators) as the A/B reference
     plan.o0_split = getenv("SURFHIP_V0_SPLIT") ? atoi(getenv("SURFHIP_V0_SPLIT")) : 44;
     plan.o0_vstrips = (oct[0].sw + 63) / 64;
     plan.o1_lds = !gather && P.noct > 1 && o1_lds_ok(P, oct[1]);
     plan.o1_v = plan.o1_lds && getenv("SURFHIP_O1_RING") == nullptr;   // A/B switch back to k_hess_o1
+    // octave-1 kernel: default k_hess_q1 (packed fp32); SURFHIP_Q1=0 selects k_hess_v1
+    plan.o1_q = getenv("SURFHIP_Q1") ? atoi(getenv("SURFHIP_Q1")) != 0 : 0;
     plan.o1_vstrips = P.noct > 1 ? (oct[1].sw + 63) / 64 : 0;
     plan.o1_nbx = P.noct > 1 ? (oct[1].sw + o1::TXS - 1) / o1::TXS : 0;
     for (int o = 0; o < kMaxOct; o++) {
@@ -1010,6 +1010,37 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
     }
     plan.hess_start[kMaxOct] = hb;
     plan.nms_start[kMaxOct] = nb;
+}
+
+std::string hessian_plan_text(const LaunchPlan& plan, const FarPlan& far, const FrameParams& P)
+{
+    std::string t;
+    auto add = [&](const char* k, int o0, int o1) {
+        if (o1 < o0) return;
+        if (!t.empty()) t += " + ";
+        t += k;
+        t += o0 == o1 ? " (octave " + std::to_string(o0) + ")"
+                      : " (octaves " + std::to_string(o0) + "-" + std::to_string(o1) + ")";
+    };
+    if (P.noct > 0) {
+        if (plan.o0_v) {
+            add(plan.o0_split == 0 ? "k_hess_v0" : "k_hess_q0", 0, 0);
+        } else if (plan.o0_lds)
+            add("k_hess_o0", 0, 0);
+    }
+    if (P.noct > 1) {
+        if (plan.o1_v) add(plan.o1_q ? "k_hess_q1" : "k_hess_v1", 1, 1);
+        else if (plan.o1_lds) add("k_hess_o1", 1, 1);
+    }
+    if (plan.vfar_n > 0) add("k_hess_vfar", 2, 1 + plan.vfar_n);
+    if (far.nfar > 0) add("k_hess_far", far.oc[0].o, far.oc[far.nfar - 1].o);
+    if (plan.hess_start[kMaxOct] > 0) {
+        int lo = -1, hi = -1;
+        for (int o = 0; o < P.noct; o++)
+            if (plan.hess_start[o + 1] > plan.hess_start[o]) { if (lo < 0) lo = o; hi = o; }
+        if (lo >= 0) add("k_hessian", lo, hi);
+    }
+    return t;
 }
 
 __device__ __forceinline__ int octave_of(const int* start, int noct, int b)
@@ -1297,59 +1328,13 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
         if (u8p) {
         const int per_xcd = (nf8 / 8) * plan.o0_vstrips;           // wave tasks per XCD
         const dim3 g(8 * ((per_xcd + v0::WAVES - 1) / v0::WAVES));
-        const int split = plan.o0_split;
-        if (split == 1) {           // scales 0-2 and 3-4 in two launches (fewer live accumulators)
-            k_hess_v0<4, 1, 0x07><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
-                                                            plan.o0_vstrips, nframes);
-            k_hess_v0<4, 1, 0x18><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
-                                                            plan.o0_vstrips, nframes);
-        } else if (split == 2) {    // scales 0-1, 2-3, 4
-            k_hess_v0<4, 1, 0x03><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
-                                                            plan.o0_vstrips, nframes);
-            k_hess_v0<4, 1, 0x0c><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
-                                                            plan.o0_vstrips, nframes);
-            k_hess_v0<4, 1, 0x10><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
-                                                            plan.o0_vstrips, nframes);
-        } else if (split == 20) {   // one wave per scale
-            const int ns = plan.o0_vstrips;
-            const int nb = (nframes >= 8 ? nf8 : nframes) * ns;
-            k_hess_s0<<<dim3(nb), s0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0], ns, nframes);
-        } else if (split == 21) {   // packed fp32, segment pairs
-            const int ns = plan.o0_vstrips;
-            const OctaveParams& q = h_oct[0];
-            const int npairs = (q.sh + 2 * f0::MAXSEG - 1) / (2 * f0::MAXSEG);
-            const int segr = (q.sh + 2 * npairs - 1) / (2 * npairs);
-            const int nb = (nframes >= 8 ? nf8 : nframes) * ns * npairs;
-            k_hess_f0<<<dim3(nb), f0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, q, ns, npairs, segr, nframes);
-        } else if (split == 30 || split == 31 || split == 32) {   // software-pipelined, branch-free
-            const dim3 gp(8 * ((per_xcd + p0::WAVES - 1) / p0::WAVES));
-            if (split == 30)
-                k_hess_p0<4, 1, false><<<gp, p0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0], plan.o0_vstrips, nframes);
-            else if (split == 31)
-                k_hess_p0<4, 1, true><<<gp, p0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0], plan.o0_vstrips, nframes);
-            else
-                k_hess_p0<6, 1, true><<<gp, p0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0], plan.o0_vstrips, nframes);
-        } else if (split >= 40 && split <= 49) {   // packed fp32 box sums, rebased local integral
-            const dim3 gq(8 * ((per_xcd + q0::WAVES - 1) / q0::WAVES));
-            auto* kq = split == 40 ? &k_hess_q0<2, 1, 1> : split == 41 ? &k_hess_q0<2, 1, 2> : split == 42 ? &k_hess_q0<2, 1, 3>
-                     : split == 43 ? &k_hess_q0<3, 1, 2> : split == 44 ? &k_hess_q0<4, 1, 2> : split == 45 ? &k_hess_q0<4, 1, 3>
-                     : &k_hess_q0<3, 1, 3>;
-            kq<<<gq, q0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0], plan.o0_vstrips, nframes);
-        } else if (split == 10) {   // experiments
-            k_hess_v0<4, 0, 0x1f><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
-                                                            plan.o0_vstrips, nframes);
-        } else if (split == 11) {
-            k_hess_v0<4, 1, 0x1f, 1><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
-                                                               plan.o0_vstrips, nframes);
-        } else if (split == 12) {
-            k_hess_v0<4, 1, 0x1f, 2><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
-                                                               plan.o0_vstrips, nframes);
-        } else if (split == 13) {
-            k_hess_v0<4, 0, 0x1f, 2><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
-                                                               plan.o0_vstrips, nframes);
-        } else {
+        if (plan.o0_split == 0) {       // A/B: the integer-accumulator kernel of round 1
             k_hess_v0<4, 1, 0x1f><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
                                                             plan.o0_vstrips, nframes);
+        } else {                        // default: packed fp32 box sums, rebased local integral
+            const dim3 gq(8 * ((per_xcd + q0::WAVES - 1) / q0::WAVES));
+            k_hess_q0<4, 1, 2><<<gq, q0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
+                                                          plan.o0_vstrips, nframes);
         }
         }
     } else if (plan.o0_lds && iip)
@@ -1357,8 +1342,12 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
     if (plan.o1_v && frames) {
         if (u8p) {
         const int per_xcd = (nf8 / 8) * plan.o1_vstrips;
-        k_hess_v1<<<dim3(8 * ((per_xcd + v1::WAVES - 1) / v1::WAVES)), v1::THREADS, 0, s>>>(
-            frames, pitch, fstride, resp, P, h_oct[1], plan.o1_vstrips, nframes);
+        if (plan.o1_q)
+            k_hess_q1<2><<<dim3(8 * ((per_xcd + q1::WAVES - 1) / q1::WAVES)), q1::THREADS, 0, s>>>(
+                frames, pitch, fstride, resp, P, h_oct[1], plan.o1_vstrips, nframes);
+        else
+            k_hess_v1<<<dim3(8 * ((per_xcd + v1::WAVES - 1) / v1::WAVES)), v1::THREADS, 0, s>>>(
+                frames, pitch, fstride, resp, P, h_oct[1], plan.o1_vstrips, nframes);
         }
     } else if (plan.o1_lds && iip)
         k_hess_o1<<<dim3(nf8 * plan.o1_nbx), o1::THREADS, 0, s>>>(ii, resp, P, h_oct[1], plan.o1_nbx, nframes);
@@ -1380,8 +1369,10 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
     }
     if (far.nfar > 0 && iip) {
         // rows of a step = R x (STRIP + 2H) columns in uint4 items: 1088 (H 144) / 1664 (H 288)
-        const hipError_t e = far.H == 144 ? launch_far<3, 144>(ii, resp, nframes, P, d_oct, far, s)
-                                          : launch_far<4, 288>(ii, resp, nframes, P, d_oct, far, s);
+        constexpr int NI144 = (farc::R * (farc::STRIP + 288) / 4 + farc::THREADS - 1) / farc::THREADS;
+        constexpr int NI288 = (farc::R * (farc::STRIP + 576) / 4 + farc::THREADS - 1) / farc::THREADS;
+        const hipError_t e = far.H == 144 ? launch_far<NI144, 144>(ii, resp, nframes, P, d_oct, far, s)
+                                          : launch_far<NI288, 288>(ii, resp, nframes, P, d_oct, far, s);
         if (e != hipSuccess) return e;
     }
     if (plan.hess_start[kMaxOct] > 0 && iip)

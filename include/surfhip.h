@@ -184,6 +184,11 @@ int surfhip_run_hessian(surfhip_detector* det, int nframes);
  * integral image read once + valid responses written. */
 long long surfhip_hessian_bytes_per_frame(surfhip_detector* det);
 
+/* The Hessian stage's kernels for this detector's launch plan, as text
+ * (e.g. "k_hess_q0 (octave 0) + k_hess_v1 (octave 1) + k_hess_far (octaves
+ * 2-3)"), NUL-terminated in buf[len]; returns the full length. */
+int surfhip_hessian_plan(surfhip_detector* det, char* buf, int len);
+
 /* Result slab for the multi-GPU all-gather, compacted to the
  * keypoints actually found by the last detect_batch:
  *   int32 {nframes, total, nfeatures (0 without descriptors), flags}
