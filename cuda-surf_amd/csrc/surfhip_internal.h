@@ -96,10 +96,8 @@ struct LaunchPlan {
 // corner row (dr) and bucketed by dr mod delta; see surfhip_kernels.hip.
 namespace farc {
 constexpr int MAXO = 3;             // far octaves on the kernel (2, 3, 4)
-#ifndef SURF_FAR_STRIP
-#define SURF_FAR_STRIP 256
-#endif
-constexpr int STRIP = SURF_FAR_STRIP; // image columns per workgroup strip
+constexpr int STRIP_W = 512;        // image columns per workgroup strip (one sample per lane at delta 8)
+constexpr int STRIP_N = 256;        // ... when the wide strip's accumulators do not fit LDS (5+ octaves)
 constexpr int R = 8;                // image rows per step (one wave each)
 constexpr int THREADS = 64 * R;
 constexpr int NA = 32;              // accumulator rows (sample rows in flight, a power of 2)
@@ -109,7 +107,7 @@ struct FarOct {
 };
 struct FarPlan {
     int nfar;                       // 0: no far kernel
-    int H, nstrips, nsteps, lds_bytes, acc_total;
+    int H, strip, nstrips, nsteps, lds_bytes, acc_total;
     FarOct oc[farc::MAXO];
 };
 // max_batch <= kGatherBatch (or SURFHIP_HESS_GATHER=1; =0 disables) puts every

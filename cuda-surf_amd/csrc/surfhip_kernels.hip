@@ -899,9 +899,10 @@ static int hessian_corners(int M, int X2, int X3, int X4, HCorner* out)
 // sampling 2: lobes 31/39/47, 63/79/95, 127/159/191, the variants compiled
 // into surfhip_far.inc) whose accumulators fit k_hess_far's LDS; any other
 // octave stays on k_hessian.
-static void make_far_plan(const FrameParams& P, const OctaveParams* oct, FarPlan& F)
+static void make_far_plan_w(const FrameParams& P, const OctaveParams* oct, FarPlan& F, int strip)
 {
     F = FarPlan{};
+    F.strip = strip;
     static const int lobes[3][3] = {{31, 39, 47}, {63, 79, 95}, {127, 159, 191}};
     int nfar = 0, hmax = 0, na = 0;
     for (int o = 2; o < P.noct && nfar < farc::MAXO; o++) {
@@ -924,7 +925,7 @@ static void make_far_plan(const FrameParams& P, const OctaveParams* oct, FarPlan
         FarOct& fo = F.oc[nfar];
         fo.o = o;
         fo.d = q.delta;
-        fo.nS = farc::STRIP / q.delta;
+        fo.nS = strip / q.delta;
         fo.drmax = drmax;
         // sample rows in flight: a row's slot is reused NA rows later, which
         // must start after the step that finalises it has ended
@@ -940,7 +941,7 @@ static void make_far_plan(const FrameParams& P, const OctaveParams* oct, FarPlan
         acc += farc::NA * 9 * F.oc[i].nS;
     }
     F.acc_total = acc;
-    const int PL = (farc::STRIP + 2 * F.H) / 8;
+    const int PL = (strip + 2 * F.H) / 8;
     F.lds_bytes = (farc::R * 8 * PL + acc) * 4;
     if (F.lds_bytes > 160 * 1024) return;
     int last = 0;
@@ -948,8 +949,21 @@ static void make_far_plan(const FrameParams& P, const OctaveParams* oct, FarPlan
         last = std::max(last, F.oc[i].d * (oct[F.oc[i].o].sh - 1) + F.oc[i].drmax);
     F.nsteps = (last + 1 + farc::R - 1) / farc::R;
     F.nsteps += F.nsteps & 1;                            // the loop runs steps in pairs
-    F.nstrips = (P.W + 1 + farc::STRIP - 1) / farc::STRIP;
+    F.nstrips = (P.W + 1 + strip - 1) / strip;
     F.nfar = nfar;
+}
+
+// The wide strip (512 columns: octave 2's samples fill a wave) where its
+// accumulators fit LDS (4 octaves: 136 KiB, one workgroup per CU), else 256
+// (5 octaves).  SURFHIP_FAR_STRIP=256 forces the narrow one (A/B).
+static void make_far_plan(const FrameParams& P, const OctaveParams* oct, FarPlan& F)
+{
+    const char* e = getenv("SURFHIP_FAR_STRIP");
+    if (!(e && atoi(e) == farc::STRIP_N)) {
+        make_far_plan_w(P, oct, F, farc::STRIP_W);
+        if (F.nfar > 0) return;
+    }
+    make_far_plan_w(P, oct, F, farc::STRIP_N);
 }
 
 // Octave o (2 or 3) of the default geometry (sampling 2: delta 8 / 16, lobes
@@ -989,7 +1003,7 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
     plan.o1_lds = !gather && P.noct > 1 && o1_lds_ok(P, oct[1]);
     plan.o1_v = plan.o1_lds && getenv("SURFHIP_O1_RING") == nullptr;   // A/B switch back to k_hess_o1
     // octave-1 kernel: default k_hess_q1 (packed fp32); SURFHIP_Q1=0 selects k_hess_v1
-    plan.o1_q = getenv("SURFHIP_Q1") ? atoi(getenv("SURFHIP_Q1")) != 0 : 0;
+    plan.o1_q = getenv("SURFHIP_Q1") ? atoi(getenv("SURFHIP_Q1")) != 0 : 1;
     plan.o1_vstrips = P.noct > 1 ? (oct[1].sw + 63) / 64 : 0;
     plan.o1_nbx = P.noct > 1 ? (oct[1].sw + o1::TXS - 1) / o1::TXS : 0;
     for (int o = 0; o < kMaxOct; o++) {
@@ -1127,10 +1141,10 @@ __global__ __launch_bounds__(256) void k_hessian(const int32_t* __restrict__ ii,
 // ----------------------------------------------------------------------
 #include "surfhip_far.inc"
 
-template <int NI, int H>
+template <int NI, int H, int ST>
 __device__ __forceinline__ void far_load(uint4 (&dst)[NI], rsrc_t I, int ip, int iH, int cs, int Y0)
 {
-    constexpr int NC4 = (farc::STRIP + 2 * H) / 4;
+    constexpr int NC4 = (ST + 2 * H) / 4;
 #pragma unroll
     for (int i = 0; i < NI; i++) {
         const int t = (int)threadIdx.x + i * farc::THREADS;
@@ -1142,10 +1156,10 @@ __device__ __forceinline__ void far_load(uint4 (&dst)[NI], rsrc_t I, int ip, int
 }
 
 // columns 4q .. 4q + 3 of a row go to planes (4q & 7) + 0..3, index q / 2
-template <int NI, int H>
+template <int NI, int H, int ST>
 __device__ __forceinline__ void far_ring_store(const uint4 (&src)[NI], uint32_t* ring)
 {
-    constexpr int NC4 = (farc::STRIP + 2 * H) / 4, PL = (farc::STRIP + 2 * H) / 8;
+    constexpr int NC4 = (ST + 2 * H) / 4, PL = (ST + 2 * H) / 8;
 #pragma unroll
     for (int i = 0; i < NI; i++) {
         const int t = (int)threadIdx.x + i * farc::THREADS;
@@ -1160,13 +1174,13 @@ __device__ __forceinline__ void far_ring_store(const uint4 (&src)[NI], uint32_t*
     }
 }
 
-template <int NI, int H>
+template <int NI, int H, int ST>
 __global__ __launch_bounds__(farc::THREADS, 2) void k_hess_far(const int32_t* __restrict__ ii,
                                                               float* __restrict__ resp, FrameParams P,
                                                               const OctaveParams* __restrict__ oct, FarPlan F,
                                                               int nframes)
 {
-    constexpr int PL = (farc::STRIP + 2 * H) / 8;
+    constexpr int PL = (ST + 2 * H) / 8;
     constexpr int ROWW = 8 * PL;
     static_assert(farc::THREADS == 64 * farc::R, "one wave per ring row");
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
@@ -1176,7 +1190,7 @@ __global__ __launch_bounds__(farc::THREADS, 2) void k_hess_far(const int32_t* __
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int X0 = strip * farc::STRIP, cs = X0 - H;
+    const int X0 = strip * ST, cs = X0 - H;
     const int nfar = F.nfar;
     uint32_t* ring = sm;
     int* acc = reinterpret_cast<int*>(sm + farc::R * ROWW);
@@ -1229,8 +1243,8 @@ __global__ __launch_bounds__(farc::THREADS, 2) void k_hess_far(const int32_t* __
     }
 
     uint4 A[NI], B[NI];
-    far_load<NI, H>(A, I, ip, iH, cs, 0);                         // rows of step 0
-    far_load<NI, H>(B, I, ip, iH, cs, farc::R);                   // rows of step 1
+    far_load<NI, H, ST>(A, I, ip, iH, cs, 0);                         // rows of step 0
+    far_load<NI, H, ST>(B, I, ip, iH, cs, farc::R);                   // rows of step 1
     // finalised responses of the previous step, stored at the start of the
     // next one: every step issues its two stores before its loads, with no
     // branch around them, so hipcc's count of outstanding VMEM ops is exact
@@ -1243,16 +1257,16 @@ __global__ __launch_bounds__(farc::THREADS, 2) void k_hess_far(const int32_t* __
     // step s + 2.
     auto step = [&](int sidx, uint4 (&cur)[NI]) {
         const int Y0 = sidx * farc::R;
-        far_ring_store<NI, H>(cur, ring);
+        far_ring_store<NI, H, ST>(cur, ring);
         buf_st_nt(Rs, poff[0], ph[0]);
         buf_st_nt(Rs, poff[1], ph[1]);
-        far_load<NI, H>(cur, I, ip, iH, cs, Y0 + 2 * farc::R);
+        far_load<NI, H, ST>(cur, I, ip, iH, cs, Y0 + 2 * farc::R);
         __syncthreads();
         // ---- accumulate every corner on the step's rows
         {
             // the step's corner groups of every far octave, dealt to the 8
             // waves by cost (tools/gen_far.py, emit_balanced)
-            far_bal<H, PL, ROWW>(nfar, (Y0 >> 3) & 3, wv, ring, lane, acc + F.oc[0].accoff + lane,
+            far_bal<H, PL, ROWW, ST>(nfar, (Y0 >> 3) & 3, wv, ring, lane, acc + F.oc[0].accoff + lane,
                                  acc + F.oc[1].accoff + lane, acc + F.oc[2].accoff + lane, Y0 >> 3, Y0 >> 4, Y0 >> 5,
                                  sh2, sh3, sh4);
         }
@@ -1304,14 +1318,16 @@ __global__ __launch_bounds__(farc::THREADS, 2) void k_hess_far(const int32_t* __
     buf_st_nt(Rs, poff[1], ph[1]);
 }
 
-template <int NI, int H>
+template <int H, int ST>
 static hipError_t launch_far(const int32_t* ii, float* resp, int nframes, const FrameParams& P,
                              const OctaveParams* d_oct, const FarPlan& far, hipStream_t s)
 {
-    hipError_t e = set_max_lds(reinterpret_cast<const void*>(&k_hess_far<NI, H>), 160 * 1024);
+    // rows of a step = R x (ST + 2H) columns in uint4 items, NI per thread
+    constexpr int NI = (farc::R * (ST + 2 * H) / 4 + farc::THREADS - 1) / farc::THREADS;
+    hipError_t e = set_max_lds(reinterpret_cast<const void*>(&k_hess_far<NI, H, ST>), 160 * 1024);
     if (e != hipSuccess) return e;
     const int nf8 = (nframes + 7) & ~7;
-    k_hess_far<NI, H><<<dim3(nf8 * far.nstrips), farc::THREADS, far.lds_bytes, s>>>(ii, resp, P, d_oct, far, nframes);
+    k_hess_far<NI, H, ST><<<dim3(nf8 * far.nstrips), farc::THREADS, far.lds_bytes, s>>>(ii, resp, P, d_oct, far, nframes);
     return hipSuccess;
 }
 
@@ -1369,10 +1385,11 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
     }
     if (far.nfar > 0 && iip) {
         // rows of a step = R x (STRIP + 2H) columns in uint4 items: 1088 (H 144) / 1664 (H 288)
-        constexpr int NI144 = (farc::R * (farc::STRIP + 288) / 4 + farc::THREADS - 1) / farc::THREADS;
-        constexpr int NI288 = (farc::R * (farc::STRIP + 576) / 4 + farc::THREADS - 1) / farc::THREADS;
-        const hipError_t e = far.H == 144 ? launch_far<NI144, 144>(ii, resp, nframes, P, d_oct, far, s)
-                                          : launch_far<NI288, 288>(ii, resp, nframes, P, d_oct, far, s);
+        const hipError_t e = far.strip == farc::STRIP_W
+                                 ? (far.H == 144 ? launch_far<144, farc::STRIP_W>(ii, resp, nframes, P, d_oct, far, s)
+                                                 : launch_far<288, farc::STRIP_W>(ii, resp, nframes, P, d_oct, far, s))
+                                 : (far.H == 144 ? launch_far<144, farc::STRIP_N>(ii, resp, nframes, P, d_oct, far, s)
+                                                 : launch_far<288, farc::STRIP_N>(ii, resp, nframes, P, d_oct, far, s));
         if (e != hipSuccess) return e;
     }
     if (plan.hess_start[kMaxOct] > 0 && iip)

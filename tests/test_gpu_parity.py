@@ -132,14 +132,24 @@ def _extreme_frame(kind, w, h, pitch):
         f[:, :w] = rng.integers(0, 256, (h, w), dtype=np.uint8)
     elif kind == "vstripes":       # 0/255 columns of period 6: large dxx, zero dyy
         f[:, :w] = np.where((np.arange(w) // 3) % 2 == 0, 255, 0).astype(np.uint8)[None, :]
+    elif kind in ("hbands", "vbands"):
+        # random-width bands varying along one axis only: one of sxx / syy is
+        # an exact 0 while the other takes both signs and sxy = 0, so the
+        # product's -0 / +0 (the reference's (float)int conversions) must
+        # come out bit for bit
+        n = h if kind == "hbands" else w
+        edges = np.cumsum(rng.integers(3, 40, n))
+        band = np.searchsorted(edges, np.arange(n), side="right")
+        vals = rng.integers(0, 256, band.max() + 1, dtype=np.uint8)[band]
+        f[:, :w] = vals[:, None] if kind == "hbands" else vals[None, :]
     elif kind == "checker":        # 7x5 blocks: large dxy
         yy, xx = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
         f[:, :w] = np.where(((yy // 5) + (xx // 7)) % 2 == 0, 255, 0).astype(np.uint8)
     return f
 
 
-@pytest.mark.parametrize("kind", ["white", "noise", "vstripes", "checker"])
-@pytest.mark.parametrize("env", ["SURFHIP_V0_SPLIT=44", "SURFHIP_V0_SPLIT=0"])
+@pytest.mark.parametrize("kind", ["white", "noise", "vstripes", "checker", "hbands", "vbands"])
+@pytest.mark.parametrize("env", ["SURFHIP_V0_SPLIT=44", "SURFHIP_V0_SPLIT=0", "SURFHIP_Q1=0"])
 def test_hessian_planes_extreme_frames(surf, orc, monkeypatch, kind, env):
     w, h = 1920, 1080
     name, _, val = env.partition("=")
@@ -156,7 +166,8 @@ def test_hessian_planes_extreme_frames(surf, orc, monkeypatch, kind, env):
 
 
 @pytest.mark.parametrize("env", ["SURFHIP_O0_RING", "SURFHIP_O1_RING", "SURFHIP_FAR_V", "SURFHIP_V0_SPLIT=0",
-                                 "SURFHIP_V0_SPLIT=44", "SURFHIP_Q1=0", "SURFHIP_Q1=1", "SURFHIP_HESS_GATHER=1"])
+                                 "SURFHIP_V0_SPLIT=44", "SURFHIP_Q1=0", "SURFHIP_Q1=1", "SURFHIP_FAR_STRIP=256",
+                                 "SURFHIP_HESS_GATHER=1"])
 @pytest.mark.parametrize("w,h,noct", [(640, 480, 4), (1920, 1080, 4)])
 def test_hessian_alternate_kernels_bit_exact(surf, orc, monkeypatch, env, w, h, noct):
     """The selectable Hessian kernels (integral-image rings for octaves 0/1,
