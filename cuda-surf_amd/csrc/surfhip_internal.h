@@ -98,9 +98,12 @@ namespace farc {
 constexpr int MAXO = 3;             // far octaves on the kernel (2, 3, 4)
 constexpr int STRIP_W = 512;        // image columns per workgroup strip (one sample per lane at delta 8)
 constexpr int STRIP_N = 256;        // ... when the wide strip's accumulators do not fit LDS (5+ octaves)
-constexpr int R = 8;                // image rows per step (one wave each)
+#ifndef SURF_FAR_R
+#define SURF_FAR_R 16
+#endif
+constexpr int R = SURF_FAR_R;       // image rows per step (one wave each; 8 or 16)
 constexpr int THREADS = 64 * R;
-constexpr int NA = 32;              // accumulator rows (sample rows in flight, a power of 2)
+constexpr int NA = 24;              // accumulator rows (sample rows in flight: <= 21 at R = 16)
 }
 struct FarOct {
     int o, d, nS, drmax, accoff;    // accoff: int offset of the [NA][9][nS] accumulators

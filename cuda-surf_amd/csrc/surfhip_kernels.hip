@@ -935,6 +935,7 @@ static void make_far_plan_w(const FrameParams& P, const OctaveParams* oct, FarPl
     if (nfar == 0) return;
     if (na > farc::NA) return;
     F.H = hmax <= 144 ? 144 : 288;                       // the two compiled halos
+    if (strip == farc::STRIP_W && F.H != 144) return;    // not compiled (and beyond LDS)
     int acc = 0;
     for (int i = 0; i < nfar; i++) {
         F.oc[i].accoff = acc;
@@ -1130,13 +1131,14 @@ __global__ __launch_bounds__(256) void k_hessian(const int32_t* __restrict__ ii,
 // Row Y carries only the corner groups of class Y mod delta, unrolled per
 // class in surfhip_far.inc (tools/gen_far.py), so every corner read is an
 // LDS immediate offset from the lane's base.
-// Wave w takes row Y0 + w of each step (R = 8 rows) for every far octave
-// and finalises (octave, scale) units w and w + 8 (unit = 3 octave + scale).
-// The ring holds one step; its rows were loaded into registers two steps
-// earlier.  Small workgroups (256-column strips, ~50 KiB LDS) so that
-// several share a CU and overlap each other's barriers; the strips of a
-// frame run on one XCD, so the column halo comes from L2 (HBM reads = one
-// integral image per frame, FETCH_SIZE).
+// A step is R = 16 integral rows (SURF_FAR_R; one wave per ring row, 1024
+// threads); the step's corner groups are dealt to the waves by cost
+// (gen_far.py), and wave w finalises (octave, scale) unit w (unit = 3 octave
+// + scale), up to R / delta sample rows per step.  The ring holds one step;
+// its rows were loaded into registers two steps earlier.  512-column strips
+// (octave 2's samples fill a wave) take 134 KiB of LDS: one 16-wave
+// workgroup per CU.  The strips of a frame run on one XCD, so the column
+// halo comes from L2 (HBM reads = one integral image per frame, FETCH_SIZE).
 // LDS: ring[R][8 planes][PL] | acc (per octave [NA][9][nS]).
 // ----------------------------------------------------------------------
 #include "surfhip_far.inc"
@@ -1151,7 +1153,12 @@ __device__ __forceinline__ void far_load(uint4 (&dst)[NI], rsrc_t I, int ip, int
         const int r = t / NC4, q = t - r * NC4;
         const int gy = Y0 + r;
         const bool ok = r < farc::R && gy < iH;
+#ifdef SURF_DIAG_FAR_NOLOAD
+        dst[i] = make_uint4((uint32_t)gy, (uint32_t)q, (uint32_t)cs, (uint32_t)ip);
+        (void)ok;
+#else
         dst[i] = buf_ld4(I, ok ? (uint32_t)(gy * ip + cs + 4 * q) * 4u : kOOB);
+#endif
     }
 }
 
@@ -1175,7 +1182,7 @@ __device__ __forceinline__ void far_ring_store(const uint4 (&src)[NI], uint32_t*
 }
 
 template <int NI, int H, int ST>
-__global__ __launch_bounds__(farc::THREADS, 2) void k_hess_far(const int32_t* __restrict__ ii,
+__global__ __launch_bounds__(farc::THREADS) void k_hess_far(const int32_t* __restrict__ ii,
                                                               float* __restrict__ resp, FrameParams P,
                                                               const OctaveParams* __restrict__ oct, FarPlan F,
                                                               int nframes)
@@ -1249,62 +1256,78 @@ __global__ __launch_bounds__(farc::THREADS, 2) void k_hess_far(const int32_t* __
     // next one: every step issues its two stores before its loads, with no
     // branch around them, so hipcc's count of outstanding VMEM ops is exact
     // and the ring write waits only for the loads of two steps back
-    uint32_t poff[2] = {kOOB, kOOB};
-    float ph[2] = {0.f, 0.f};
+    // MR: sample rows a unit may finalise per step (R / delta, delta >= 8)
+    constexpr int MR = farc::R / 8;
+    uint32_t poff[2][MR];
+    float ph[2][MR];
+#pragma unroll
+    for (int k = 0; k < 2; k++)
+#pragma unroll
+        for (int m = 0; m < MR; m++) { poff[k][m] = kOOB; ph[k][m] = 0.f; }
 
-    // One step: rows Y0 .. Y0 + 7.  `cur` (this step's rows, loaded two
+    // One step: rows Y0 .. Y0 + R - 1.  `cur` (this step's rows, loaded two
     // steps earlier) goes to the ring, then `cur` receives the loads for
     // step s + 2.
     auto step = [&](int sidx, uint4 (&cur)[NI]) {
         const int Y0 = sidx * farc::R;
         far_ring_store<NI, H, ST>(cur, ring);
-        buf_st_nt(Rs, poff[0], ph[0]);
-        buf_st_nt(Rs, poff[1], ph[1]);
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+#pragma unroll
+            for (int m = 0; m < MR; m++) buf_st_nt(Rs, poff[k][m], ph[k][m]);
         far_load<NI, H, ST>(cur, I, ip, iH, cs, Y0 + 2 * farc::R);
         __syncthreads();
         // ---- accumulate every corner on the step's rows
         {
-            // the step's corner groups of every far octave, dealt to the 8
+            // the step's corner groups of every far octave, dealt to the R
             // waves by cost (tools/gen_far.py, emit_balanced)
-            far_bal<H, PL, ROWW, ST>(nfar, (Y0 >> 3) & 3, wv, ring, lane, acc + F.oc[0].accoff + lane,
-                                 acc + F.oc[1].accoff + lane, acc + F.oc[2].accoff + lane, Y0 >> 3, Y0 >> 4, Y0 >> 5,
-                                 sh2, sh3, sh4);
+#ifndef SURF_DIAG_FAR_NOACC
+            far_bal<H, PL, ROWW, ST>(nfar, sidx, wv, ring, lane, acc + F.oc[0].accoff + lane,
+                                     acc + F.oc[1].accoff + lane, acc + F.oc[2].accoff + lane, Y0 >> 3, Y0 >> 4,
+                                     Y0 >> 5, sh2, sh3, sh4);
+#endif
         }
         __syncthreads();
-        // ---- finalise the sample row (of each far octave) whose last corner
-        // row has passed: at most one per octave per step (delta >= R); wave
-        // w takes units (octave, scale) w and w + 8
+        // ---- finalise the sample rows (of each far octave) whose last corner
+        // row has passed: at most R / delta per octave per step; wave w takes
+        // units (octave, scale) w and w + R
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             const FinUnit& u = fu[k];
-            uint32_t off = kOOB;
-            float h = 0.f;
-            if (u.on) {
-                const int iy = next_iy[u.oi];
-                if (iy < u.sh && u.d * iy + u.drmax <= Y0 + farc::R - 1 && lane < u.nS) {
-                    int* a = acc + u.accoff + (iy & (farc::NA - 1)) * 9 * u.nS;
-                    const int32_t sxx = a[0], syy = a[u.nS], sxy = a[2 * u.nS];
-                    a[0] = 0;
-                    a[u.nS] = 0;
-                    a[2 * u.nS] = 0;
-                    const float rr = INV255 * INV255;
-                    const float dxx = (float)sxx;
-                    const float dyy = (float)syy;
-                    const float dxy = 0.6f * (float)sxy;
-                    const float pp = dxx * dyy;
-                    const float q2 = dxy * dxy;
-                    const bool v = iy >= u.b1 && iy < u.sh - u.b1 && u.colok;
-                    h = v ? (rr * (pp - q2)) * u.norm : 0.f;
-                    if (u.colin) off = (uint32_t)(u.pbase + iy * u.sp) * 4u;
+#pragma unroll
+            for (int m = 0; m < MR; m++) {
+                uint32_t off = kOOB;
+                float h = 0.f;
+                if (u.on) {
+                    const int iy = next_iy[u.oi] + m;
+                    if (iy < u.sh && u.d * iy + u.drmax <= Y0 + farc::R - 1 && lane < u.nS) {
+                        int* a = acc + u.accoff + ((unsigned)iy % farc::NA) * 9 * u.nS;
+                        const int32_t sxx = a[0], syy = a[u.nS], sxy = a[2 * u.nS];
+                        a[0] = 0;
+                        a[u.nS] = 0;
+                        a[2 * u.nS] = 0;
+                        const float rr = INV255 * INV255;
+                        const float dxx = (float)sxx;
+                        const float dyy = (float)syy;
+                        const float dxy = 0.6f * (float)sxy;
+                        const float pp = dxx * dyy;
+                        const float q2 = dxy * dxy;
+                        const bool v = iy >= u.b1 && iy < u.sh - u.b1 && u.colok;
+                        h = v ? (rr * (pp - q2)) * u.norm : 0.f;
+                        if (u.colin) off = (uint32_t)(u.pbase + iy * u.sp) * 4u;
+                    }
                 }
+                poff[k][m] = off;
+                ph[k][m] = h;
             }
-            poff[k] = off;
-            ph[k] = h;
         }
         // every wave tracks every octave's next row identically
 #pragma unroll
         for (int oi = 0; oi < farc::MAXO; oi++) {
-            if (oi < nfar && next_iy[oi] < osh[oi] && odr[oi] * next_iy[oi] + odm[oi] <= Y0 + farc::R - 1) next_iy[oi]++;
+#pragma unroll
+            for (int m = 0; m < MR; m++)
+                if (oi < nfar && next_iy[oi] < osh[oi] && odr[oi] * next_iy[oi] + odm[oi] <= Y0 + farc::R - 1)
+                    next_iy[oi]++;
         }
         // no barrier here: the next step's ring writes come after every wave
         // passed this step's second barrier (all reads of the ring done), and
@@ -1314,8 +1337,10 @@ __global__ __launch_bounds__(farc::THREADS, 2) void k_hess_far(const int32_t* __
         step(s2, A);
         step(s2 + 1, B);
     }
-    buf_st_nt(Rs, poff[0], ph[0]);
-    buf_st_nt(Rs, poff[1], ph[1]);
+#pragma unroll
+    for (int k = 0; k < 2; k++)
+#pragma unroll
+        for (int m = 0; m < MR; m++) buf_st_nt(Rs, poff[k][m], ph[k][m]);
 }
 
 template <int H, int ST>
@@ -1385,11 +1410,10 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
     }
     if (far.nfar > 0 && iip) {
         // rows of a step = R x (STRIP + 2H) columns in uint4 items: 1088 (H 144) / 1664 (H 288)
-        const hipError_t e = far.strip == farc::STRIP_W
-                                 ? (far.H == 144 ? launch_far<144, farc::STRIP_W>(ii, resp, nframes, P, d_oct, far, s)
-                                                 : launch_far<288, farc::STRIP_W>(ii, resp, nframes, P, d_oct, far, s))
-                                 : (far.H == 144 ? launch_far<144, farc::STRIP_N>(ii, resp, nframes, P, d_oct, far, s)
-                                                 : launch_far<288, farc::STRIP_N>(ii, resp, nframes, P, d_oct, far, s));
+        // (the wide strip only with the 144 halo: make_far_plan_w)
+        const hipError_t e = far.strip == farc::STRIP_W ? launch_far<144, farc::STRIP_W>(ii, resp, nframes, P, d_oct, far, s)
+                             : far.H == 144             ? launch_far<144, farc::STRIP_N>(ii, resp, nframes, P, d_oct, far, s)
+                                                        : launch_far<288, farc::STRIP_N>(ii, resp, nframes, P, d_oct, far, s);
         if (e != hipSuccess) return e;
     }
     if (plan.hess_start[kMaxOct] > 0 && iip)

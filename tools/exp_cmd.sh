@@ -2,6 +2,6 @@ set -u
 cd /tmp && export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-SURFHIP_Q1=1 timeout -k 10 120 python -u tools/dbg_planes.py 1920 1080 4 7 || exit 1
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "hessian" > gpurun_out/e3_pytest.log 2>&1 || { tail -30 gpurun_out/e3_pytest.log; exit 1; }
-tail -1 gpurun_out/e3_pytest.log
+bash tools/diag_run.sh k_hess_far default r8 noacc noload -- --hessian-only
+for v in default r8 noacc noload; do echo $v; python3 tools/kstats.py gpurun_out/dg_$v/run_kernel_trace.csv k_hess_far; done
+bash tools/pmc_kern.sh sqf k_hess_far "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU" -- --hessian-only

@@ -12,10 +12,12 @@ grouped by (dr, slot) and bucketed by rho = dr mod delta: integral row Y
 contributes exactly the groups of class Y mod delta, to sample row
 iy = (Y - dr) / delta.
 
-For each (octave variant, rho) this emits one device function that reads
-the group's corners from the residue-plane LDS row (plane = column mod 8,
-so lane j's corner is a compile-time offset from the lane's base) and adds
-each group's weighted sum into its LDS accumulator.
+The corner groups of a step's rows are dealt to the workgroup's waves by
+cost (emit_balanced); each wave reads its groups' corners from the
+residue-plane LDS ring (plane = column mod 8, so lane j's corner is a
+compile-time offset from the lane's base) and adds each group's weighted
+sum into its LDS accumulator.  Programs are emitted for 8- and 16-row steps
+(SURF_FAR_R selects one at compile time).
 """
 import os
 import sys
@@ -68,47 +70,46 @@ def groups(oct_):
     return d, out
 
 
-def emit():
-    lines = ["// Generated by tools/gen_far.py -- do not edit.",
-             "// Far-octave corner programs for k_hess_far (see the generator's docstring).",
-             ""]
-    lines.extend(emit_balanced())
-    return "\n".join(lines) + "\n"
-
-
 OCTS = (2, 3, 4)
-NWAVES = 8
+RS = (8, 16)            # rows per step (= waves per workgroup) variants, selected by SURF_FAR_R
 
 
-def emit_balanced():
-    """Per-wave programs: a step's 8 ring rows carry, per far octave, the
-    corner groups of 8 residues; wave w of the step used to take row w
-    (residue costs differ up to 9x, so the step waited on the busiest wave).
-    Here every (octave, row, group) item of a step phase is dealt to the 8
-    waves by cost (greedy, largest first); each wave reads its items' rows
-    from the ring and adds into the LDS accumulators (ds_add, so waves may
-    share one)."""
-    out = ["", "// ---- load-balanced per-wave programs (see emit_balanced)"]
+def emit_balanced(R):
+    """Per-wave programs for steps of R integral rows (one ring row per wave):
+    a step carries, per far octave of delta d, the corner groups of the
+    residues (R ph + j) mod d of its rows j (ph: the step's phase when d > R).
+    Every (octave, row, group) item of a step phase is dealt to the R waves
+    by cost (greedy, largest first: residue costs differ up to 9x, so a
+    wave-per-row split waited on the busiest row); each wave reads its items'
+    rows from the ring and adds into the LDS accumulators (ds_add, so waves
+    may share one).  Sample row of an item: i + k with i = Y0 / d (floor) and
+    k = ((R ph) mod d + j - dr) / d; accumulator row (i + k) mod NA."""
+    nw = R
+    out = ["", f"// ---- load-balanced per-wave programs, {R} rows per step (see emit_balanced)"]
     for nfar in (1, 2, 3):
-        nph = 1 << (nfar - 1)
+        dmax = VARIANTS[OCTS[nfar - 1]][0]
+        nph = max(1, dmax // R)
         for ph in range(nph):
             items = []
             for oi in range(nfar):
                 o = OCTS[oi]
                 d, g = groups(o)
-                for j in range(8):
-                    rho = (8 * ph + j) % d
+                off = (R * ph) % d
+                for j in range(R):
+                    rho = (off + j) % d
                     for (dr, slot, cs) in g.get(rho, []):
-                        items.append((len(cs) + 1, oi, d, j, rho, dr, slot, cs))
+                        k = (off + j - dr) // d
+                        assert (off + j - dr) % d == 0
+                        items.append((len(cs) + 1, oi, d, j, k, dr, slot, cs))
             items.sort(key=lambda t: (-t[0], t[1], t[3], t[5], t[6]))
-            load = [0] * NWAVES
-            bins = [[] for _ in range(NWAVES)]
+            load = [0] * nw
+            bins = [[] for _ in range(nw)]
             for it in items:
-                w = min(range(NWAVES), key=lambda i: (load[i], i))
+                w = min(range(nw), key=lambda i: (load[i], i))
                 load[w] += it[0]
                 bins[w].append(it)
             out.append(f"// nfar {nfar} phase {ph}: wave loads {load}")
-            for w in range(NWAVES):
+            for w in range(nw):
                 out.append("template <int H, int PL, int ROWW, int ST>")
                 out.append(f"__device__ __forceinline__ void far_bal_n{nfar}_p{ph}_w{w}(const uint32_t* __restrict__ ring, "
                            "int lane, int* __restrict__ a0, int* __restrict__ a1, int* __restrict__ a2, int i0, int i1, "
@@ -122,7 +123,7 @@ def emit_balanced():
                     ls = d // 8
                     out.append(f"    if (lane < ST / {d}) {{")
                     out.append(f"        const uint32_t* rb = ring + {ls} * lane;")
-                    for n, (_, _, _, j, rho, dr, slot, cs) in enumerate(mine):
+                    for n, (_, _, _, j, k, dr, slot, cs) in enumerate(mine):
                         terms = []
                         for dc, wt in cs:
                             v = f"rb[{j} * ROWW + ((H + ({dc})) & 7) * PL + ((H + ({dc})) >> 3)]"
@@ -137,30 +138,44 @@ def emit_balanced():
                         expr = " ".join(terms)
                         expr = expr[2:] if expr.startswith("+ ") else "0u " + expr
                         out.append(f"        const uint32_t t{n} = {expr};")
-                    for n, (_, _, _, j, rho, dr, slot, cs) in enumerate(mine):
-                        k = (rho - dr) // d
+                    for n, (_, _, _, j, k, dr, slot, cs) in enumerate(mine):
                         out.append(f"        if ((unsigned)(i{oi} + ({k})) < (unsigned)s{oi})")
-                        out.append(f"            atomicAdd(a{oi} + (((i{oi} + ({k})) & (farc::NA - 1)) * 9 + {slot}) * "
+                        out.append(f"            atomicAdd(a{oi} + (((unsigned)(i{oi} + ({k})) % farc::NA) * 9 + {slot}) * "
                                    f"(ST / {d}), (int)t{n});")
                     out.append("    }")
                 out.append("}")
                 out.append("")
-    # dispatcher
+    # dispatcher: step index Y0 / R gives the phase
     out.append("template <int H, int PL, int ROWW, int ST>")
-    out.append("__device__ __forceinline__ void far_bal(int nfar, int phase, int w, const uint32_t* __restrict__ ring, "
+    out.append("__device__ __forceinline__ void far_bal(int nfar, int step, int w, const uint32_t* __restrict__ ring, "
                "int lane, int* a0, int* a1, int* a2, int i0, int i1, int i2, int s0, int s1, int s2)")
     out.append("{")
-    out.append("    switch ((nfar - 1) * 32 + (phase & ((1 << (nfar - 1)) - 1)) * 8 + w) {")
+    out.append(f"    const int ph = step & ((nfar == 3 ? {max(1, 32 // R)} : nfar == 2 ? {max(1, 16 // R)} : 1) - 1);")
+    out.append(f"    switch (((nfar - 1) * 4 + ph) * {nw} + w) {{")
     for nfar in (1, 2, 3):
-        for ph in range(1 << (nfar - 1)):
-            for w in range(NWAVES):
-                out.append(f"    case {(nfar - 1) * 32 + ph * 8 + w}: far_bal_n{nfar}_p{ph}_w{w}<H, PL, ROWW, ST>(ring, lane, "
+        dmax = VARIANTS[OCTS[nfar - 1]][0]
+        for ph in range(max(1, dmax // R)):
+            for w in range(nw):
+                out.append(f"    case {((nfar - 1) * 4 + ph) * nw + w}: far_bal_n{nfar}_p{ph}_w{w}<H, PL, ROWW, ST>(ring, lane, "
                            "a0, a1, a2, i0, i1, i2, s0, s1, s2); break;")
     out.append("    default: break;")
     out.append("    }")
     out.append("}")
     out.append("")
     return out
+
+
+def emit():
+    lines = ["// Generated by tools/gen_far.py -- do not edit.",
+             "// Far-octave corner programs for k_hess_far (see the generator's docstring).",
+             ""]
+    for i, R in enumerate(RS):
+        lines.append(("#if" if i == 0 else "#elif") + f" SURF_FAR_R == {R}")
+        lines.extend(emit_balanced(R))
+    lines.append("#else")
+    lines.append("#error \"SURF_FAR_R: no corner programs generated for this step height\"")
+    lines.append("#endif")
+    return "\n".join(lines) + "\n"
 
 
 if __name__ == "__main__":
