@@ -88,6 +88,7 @@ struct LaunchPlan {
     int o1_lds;                     // octave 1 on the LDS ring (k_hess_o1)
     int o1_v, o1_vstrips;           // octave 1 on the u8 vertical-streaming kernel (k_hess_v1)
     int o1_q;                       // ... its packed-fp32 variant (k_hess_q1)
+    int o01;                        // q0 and q1 in one launch (k_hess_q01)
     int vfar_n;                     // octaves 2 .. 1 + vfar_n on k_hess_vfar (u8 vertical streaming)
     int o1_nbx;
 };

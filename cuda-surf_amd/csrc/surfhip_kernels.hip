@@ -1006,6 +1006,8 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
     // octave-1 kernel: default k_hess_q1 (packed fp32); SURFHIP_Q1=0 selects k_hess_v1
     plan.o1_q = getenv("SURFHIP_Q1") ? atoi(getenv("SURFHIP_Q1")) != 0 : 1;
     plan.o1_vstrips = P.noct > 1 ? (oct[1].sw + 63) / 64 : 0;
+    // octaves 0 and 1 in one launch (k_hess_q01); SURFHIP_Q01=0 launches them apart
+    plan.o01 = getenv("SURFHIP_Q01") ? atoi(getenv("SURFHIP_Q01")) != 0 : 1;
     plan.o1_nbx = P.noct > 1 ? (oct[1].sw + o1::TXS - 1) / o1::TXS : 0;
     for (int o = 0; o < kMaxOct; o++) {
         plan.hess_start[o] = hb;
@@ -1038,12 +1040,14 @@ std::string hessian_plan_text(const LaunchPlan& plan, const FarPlan& far, const 
                       : " (octaves " + std::to_string(o0) + "-" + std::to_string(o1) + ")";
     };
     if (P.noct > 0) {
-        if (plan.o0_v) {
+        if (plan.o01 && plan.o0_v && plan.o0_split != 0 && P.noct > 1 && plan.o1_v && plan.o1_q) {
+            add("k_hess_q01", 0, 1);
+        } else if (plan.o0_v) {
             add(plan.o0_split == 0 ? "k_hess_v0" : "k_hess_q0", 0, 0);
         } else if (plan.o0_lds)
             add("k_hess_o0", 0, 0);
     }
-    if (P.noct > 1) {
+    if (P.noct > 1 && !(plan.o01 && plan.o0_v && plan.o0_split != 0 && plan.o1_v && plan.o1_q)) {
         if (plan.o1_v) add(plan.o1_q ? "k_hess_q1" : "k_hess_v1", 1, 1);
         else if (plan.o1_lds) add("k_hess_o1", 1, 1);
     }
@@ -1365,7 +1369,15 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
     // integral image (the two may run on different streams)
     if (!frames) parts = 3;
     const bool u8p = (parts & 1) != 0, iip = (parts & 2) != 0;
-    if (plan.o0_v && frames) {
+    const bool merged = plan.o01 && plan.o0_v && plan.o0_split != 0 && plan.o1_v && plan.o1_q && frames;
+    if (merged && u8p) {
+        const int nb0 = 8 * (((nf8 / 8) * plan.o0_vstrips + q0::WAVES - 1) / q0::WAVES);
+        const int nb1 = 8 * (((nf8 / 8) * plan.o1_vstrips + q1::WAVES - 1) / q1::WAVES);
+        k_hess_q01<<<dim3(nb0 + nb1), q0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0], h_oct[1],
+                                                           plan.o0_vstrips, plan.o1_vstrips, nb0, nframes);
+    }
+    if (merged) {
+    } else if (plan.o0_v && frames) {
         if (u8p) {
         const int per_xcd = (nf8 / 8) * plan.o0_vstrips;           // wave tasks per XCD
         const dim3 g(8 * ((per_xcd + v0::WAVES - 1) / v0::WAVES));
@@ -1380,7 +1392,8 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
         }
     } else if (plan.o0_lds && iip)
         k_hess_o0<<<dim3(nf8 * plan.o0_nbx), o0::THREADS, 0, s>>>(ii, resp, P, h_oct[0], plan.o0_nbx, nframes);
-    if (plan.o1_v && frames) {
+    if (merged) {
+    } else if (plan.o1_v && frames) {
         if (u8p) {
         const int per_xcd = (nf8 / 8) * plan.o1_vstrips;
         if (plan.o1_q)

@@ -166,7 +166,7 @@ def test_hessian_planes_extreme_frames(surf, orc, monkeypatch, kind, env):
 
 
 @pytest.mark.parametrize("env", ["SURFHIP_O0_RING", "SURFHIP_O1_RING", "SURFHIP_FAR_V", "SURFHIP_V0_SPLIT=0",
-                                 "SURFHIP_V0_SPLIT=44", "SURFHIP_Q1=0", "SURFHIP_Q1=1", "SURFHIP_FAR_STRIP=256",
+                                 "SURFHIP_V0_SPLIT=44", "SURFHIP_Q1=0", "SURFHIP_Q1=1", "SURFHIP_Q01=0", "SURFHIP_FAR_STRIP=256",
                                  "SURFHIP_HESS_GATHER=1"])
 @pytest.mark.parametrize("w,h,noct", [(640, 480, 4), (1920, 1080, 4)])
 def test_hessian_alternate_kernels_bit_exact(surf, orc, monkeypatch, env, w, h, noct):

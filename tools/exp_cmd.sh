@@ -2,6 +2,9 @@ set -u
 cd /tmp && export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-bash tools/diag_run.sh k_hess_far default r8 noacc noload -- --hessian-only
-for v in default r8 noacc noload; do echo $v; python3 tools/kstats.py gpurun_out/dg_$v/run_kernel_trace.csv k_hess_far; done
-bash tools/pmc_kern.sh sqf k_hess_far "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU" -- --hessian-only
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "hessian" > gpurun_out/e9_pytest.log 2>&1 || { tail -30 gpurun_out/e9_pytest.log; exit 1; }
+tail -1 gpurun_out/e9_pytest.log
+for c in 1 0 1 0; do
+SURFHIP_Q01=$c timeout -k 10 200 python3 bench.py --steps 20 --warmup 3 --no-cpu --hessian-only > gpurun_out/hq_$c.json 2> gpurun_out/hq_$c.err || { tail -5 gpurun_out/hq_$c.err; exit 1; }
+python3 -c "import json;d=json.load(open('gpurun_out/hq_$c.json'));print('q01 $c', d['roofline']['launch_ms'], d['roofline']['frac'], d['roofline']['kernel'])"
+done
