@@ -69,6 +69,7 @@ struct surfhip_detector {
     int* cand_count = nullptr;
     uint32_t* scan_key = nullptr;       // NMS survivors awaiting interpolation
     uint32_t* scan_src = nullptr;
+    float* scan_cube = nullptr;         // the survivors' fit inputs (kCubeCap per scan item)
     int* item_count = nullptr;          // survivors per NMS scan item
     int* item_off = nullptr;            // their exclusive prefix (+ total)
     int nitems = 0;                     // scan items per frame
@@ -386,7 +387,7 @@ static int derive(surfhip_detector* d)
 static void free_all(surfhip_detector* d)
 {
     void* ptrs[] = {d->d_oct, d->ii, d->resp, d->colsum, d->cand, d->keys, d->gscratch, d->cand_count,
-                    d->scan_key, d->scan_src, d->item_count, d->item_off,
+                    d->scan_key, d->scan_src, d->scan_cube, d->item_count, d->item_off,
                     d->offsets, d->order, d->status, d->pts1, d->desc1, d->count1, d->dbl};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -452,6 +453,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     d->nitems = d->plan.nms_start[kMaxOct] * 4;
     ALLOC(d->scan_key, B * (size_t)d->nitems * kItemCap * sizeof(uint32_t));
     ALLOC(d->scan_src, B * (size_t)d->nitems * kItemCap * sizeof(uint32_t));
+    ALLOC(d->scan_cube, B * (size_t)d->nitems * kCubeCap * kCubeF * sizeof(float));
     ALLOC(d->item_count, B * (size_t)d->nitems * sizeof(int));
     // prefix (nitems + 1) followed by the scan's per-chunk totals
     ALLOC(d->item_off, (2 * B * (size_t)d->nitems + 64) * sizeof(int));
@@ -596,7 +598,8 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
                               d->plan, d->far, s, 1));
         HIPCHK(hipStreamWaitEvent(s, d->join, 0));
     }
-    HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->scan_key, d->scan_src, d->item_count,
+    HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->scan_key, d->scan_src, d->scan_cube,
+                      d->item_count,
                       d->item_off, d->cand, d->keys, d->cand_count, d->cap, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[3], s));
     HIPCHK(launch_sort(d->cand, d->keys, d->gscratch, d->cand_count, d->item_off, d->plan.nms_start[kMaxOct] * 4,

@@ -36,6 +36,8 @@ inline long long integral_bands(int H, int max_batch)
 }
 constexpr int kScanRows = 16;       // NMS block rows per scan workgroup (4 per wave)
 constexpr int kItemCap = 64 * (kScanRows / 4);   // 2x2x2 blocks (= survivor slots) per scan item
+constexpr int kCubeCap = 8;         // survivors per scan item whose fit inputs the scan records
+constexpr int kCubeF = 20;          // floats per record (fit_quad's 19 responses + pad)
 
 // Per-octave geometry and Hessian/NMS parameters, exactly as the reference
 // host code derives them (surf.cpp:240-292, surfd.cu:2844-2865, 3062-3076).
@@ -132,8 +134,8 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
 // each item owns kItemCap survivor slots (no atomics in the scan).
 hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,
                       const OctaveParams* d_oct, const LaunchPlan& plan, uint32_t* scan_key, uint32_t* scan_src,
-                      int* item_count, int* item_off, surfhip_point* cand, uint32_t* keys, int* cand_count, int cap,
-                      hipStream_t s);
+                      float* scan_cube, int* item_count, int* item_off, surfhip_point* cand, uint32_t* keys,
+                      int* cand_count, int cap, hipStream_t s);
 hipError_t launch_sort(const surfhip_point* cand, const uint32_t* keys, uint64_t* gscratch,
                        const int* cand_count, const int* soff, int items_per_frame, int cap, int nframes,
                        surfhip_point* out, int max_pts, int* out_count, int* offsets, int* order, int* status,

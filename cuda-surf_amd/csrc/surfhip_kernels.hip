@@ -1499,11 +1499,16 @@ struct OctView {
     }
 };
 
-__device__ float fit_quad(const OctView& V, float (&off)[3], int s, int r, int c)
+// fitQuadrat (surfd.cu:942-988) on the 19 responses it reads around (s, r,
+// c): v = {c, s+1, s-1, r+1, r-1, c+1, c-1, (s+1, r+1), (s+1, r-1),
+// (s-1, r+1), (s-1, r-1), (s+1, c+1), (s+1, c-1), (s-1, c+1), (s-1, c-1),
+// (r+1, c+1), (r+1, c-1), (r-1, c+1), (r-1, c-1)} (the NMS scan writes this
+// record for its survivors, k_nms_scan)
+__device__ float fit_quad_v(const float* v, float (&off)[3])
 {
-    const float c0 = V(s, r, c);
-    const float nx0 = V(s + 1, r, c), pv0 = V(s - 1, r, c);
-    const float cnr = V(s, r + 1, c), cpr = V(s, r - 1, c), cnc = V(s, r, c + 1), cpc = V(s, r, c - 1);
+    const float c0 = v[0];
+    const float nx0 = v[1], pv0 = v[2];
+    const float cnr = v[3], cpr = v[4], cnc = v[5], cpc = v[6];
     float g[3], H[3][3];
     g[0] = (nx0 - pv0) * 0.5f;
     g[1] = (cnr - cpr) * 0.5f;
@@ -1512,9 +1517,9 @@ __device__ float fit_quad(const OctView& V, float (&off)[3], int s, int r, int c
     H[0][0] = (pv0 + nx0) - temp;
     H[1][1] = (cnr + cpr) - temp;
     H[2][2] = (cnc + cpc) - temp;
-    H[0][1] = ((V(s + 1, r + 1, c) - V(s + 1, r - 1, c)) - (V(s - 1, r + 1, c) - V(s - 1, r - 1, c))) * 0.25f;
-    H[0][2] = ((V(s + 1, r, c + 1) - V(s + 1, r, c - 1)) - (V(s - 1, r, c + 1) - V(s - 1, r, c - 1))) * 0.25f;
-    H[1][2] = ((V(s, r + 1, c + 1) - V(s, r + 1, c - 1)) - (V(s, r - 1, c + 1) - V(s, r - 1, c - 1))) * 0.25f;
+    H[0][1] = ((v[7] - v[8]) - (v[9] - v[10])) * 0.25f;
+    H[0][2] = ((v[11] - v[12]) - (v[13] - v[14])) * 0.25f;
+    H[1][2] = ((v[15] - v[16]) - (v[17] - v[18])) * 0.25f;
     H[1][0] = H[0][1];
     H[2][0] = H[0][2];
     H[2][1] = H[1][2];
@@ -1524,6 +1529,18 @@ __device__ float fit_quad(const OctView& V, float (&off)[3], int s, int r, int c
     solve3(off, H);
     const float dot = (off[0] * g[0] + off[1] * g[1]) + off[2] * g[2];
     return c0 + 0.5f * dot;
+}
+
+__device__ float fit_quad(const OctView& V, float (&off)[3], int s, int r, int c)
+{
+    const float v[19] = {V(s, r, c),
+                         V(s + 1, r, c),         V(s - 1, r, c),
+                         V(s, r + 1, c),         V(s, r - 1, c),
+                         V(s, r, c + 1),         V(s, r, c - 1),
+                         V(s + 1, r + 1, c),     V(s + 1, r - 1, c),     V(s - 1, r + 1, c),     V(s - 1, r - 1, c),
+                         V(s + 1, r, c + 1),     V(s + 1, r, c - 1),     V(s - 1, r, c + 1),     V(s - 1, r, c - 1),
+                         V(s, r + 1, c + 1),     V(s, r + 1, c - 1),     V(s, r - 1, c + 1),     V(s, r - 1, c - 1)};
+    return fit_quad_v(v, off);
 }
 
 // getTrace (surfd.cu:369-377).  makePoint builds this box from the
@@ -1554,8 +1571,11 @@ __device__ __forceinline__ int32_t trace_sign(const uint32_t* __restrict__ I, in
 
 // Sub-pixel interpolation + acceptance + makePoint (surfd.cu:794-831,
 // 942-1022) for one NMS survivor.
+// cube: the scan's record of the 19 responses around (s, r, c) (nullptr:
+// read them from the planes)
 __device__ bool nms_fit_point(const uint32_t* __restrict__ I, const OctView& V, const FrameParams& P,
-                              const OctaveParams& q, int o, int s, int r, int c, surfhip_point& pt)
+                              const OctaveParams& q, int o, int s, int r, int c, const float4* cube,
+                              surfhip_point& pt)
 {
     const int sw = q.sw, sh = q.sh;
     float off[3] = {0.f, 0.f, 0.f};
@@ -1563,7 +1583,17 @@ __device__ bool nms_fit_point(const uint32_t* __restrict__ I, const OctView& V, 
     int newr = r, newc = c;
     for (int mv = 0; mv < 5; mv++) {
         r = newr; c = newc;
-        strength = fit_quad(V, off, s, r, c);
+        if (mv == 0 && cube) {
+            float v[20];
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                const float4 t = cube[k];
+                v[4 * k] = t.x; v[4 * k + 1] = t.y; v[4 * k + 2] = t.z; v[4 * k + 3] = t.w;
+            }
+            strength = fit_quad_v(v, off);
+        } else {
+            strength = fit_quad(V, off, s, r, c);
+        }
         const int bs = q.borders[s];
         if (off[1] > 0.6f && r < sh - bs) newr++;
         if (off[1] < -0.6f && r > bs) newr--;
@@ -1644,6 +1674,7 @@ __device__ __forceinline__ int wave_append(bool ok, int* counter)
 __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, const FrameParams& P,
                                               const OctaveParams* __restrict__ oct, const LaunchPlan& plan,
                                               uint32_t* __restrict__ scan_key, uint32_t* __restrict__ scan_src,
+                                              float* __restrict__ scan_cube,
                                               int* __restrict__ item_count, int nitems_frame, int f, int gb, int wv,
                                               float* sbest, uint32_t* sinfo)
 {
@@ -1666,6 +1697,7 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
     const size_t item = ((size_t)f * nitems_frame + gb) * 4 + wv;
     uint32_t* rkey = scan_key + item * kItemCap;
     uint32_t* rsrc_ = scan_src + item * kItemCap;
+    float* rcube = scan_cube + item * kCubeCap * kCubeF;
     int nsurv = 0;
     // ---- a pass's 2x2x2 block loads, all issued before any use
     float v[2][NU][8];
@@ -1726,30 +1758,34 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
         for (int c0 = 0; c0 < ncand; c0 += 64) {
             const int ci = c0 + (int)lane_id();
             bool ok = false;
-            int s = 0, r = 0, c = 0, xx = 0, y = 0;
+            int s = 0, r = 0, c = 0, xx = 0, y = 0, ds = 1, dr = 1, dc = 1;
+            float best = 0.f, nb[19];
             if (ci < ncand) {
-                const float best = sbest[ci];
+                best = sbest[ci];
                 const uint32_t info = sinfo[ci];
                 const int u = (int)(info >> 9), cas = (int)((info >> 6) & 7u);
                 xx = bx0 + (int)(info & 63u);
                 y = y0 + 4 * u;
                 const int i = mb + y * 2, jx = mb + xx * 2;
                 s = k + (cas >> 2); r = i + ((cas >> 1) & 1); c = jx + (cas & 1);
-                const int ds = (cas >> 2) ? 1 : -1, dr = ((cas >> 1) & 1) ? 1 : -1, dc = (cas & 1) ? 1 : -1;
+                ds = (cas >> 2) ? 1 : -1; dr = ((cas >> 1) & 1) ? 1 : -1; dc = (cas & 1) ? 1 : -1;
                 const int so = s + ds, si = s - ds;
                 const int rn = r + dr, rp = r - dr, cn = c + dc;
                 // the 19 neighbours outside the block, ties survive (surfd.cu:757-792);
                 // all loads issued before any compare
-                const float nb[19] = {V(so, rp, c - 1), V(so, rp, c), V(so, rp, c + 1),
-                                      V(so, r, c - 1),  V(so, r, c),  V(so, r, c + 1),
-                                      V(so, rn, c - 1), V(so, rn, c), V(so, rn, c + 1),
-                                      V(s, rn, c - 1),  V(s, rn, c),  V(s, rn, c + 1),
-                                      V(s, r, cn),      V(s, rp, cn),
-                                      V(si, rn, c - 1), V(si, rn, c), V(si, rn, c + 1),
-                                      V(si, rp, cn),    V(si, r, cn)};
+                const float nbv[19] = {V(so, rp, c - 1), V(so, rp, c), V(so, rp, c + 1),
+                                       V(so, r, c - 1),  V(so, r, c),  V(so, r, c + 1),
+                                       V(so, rn, c - 1), V(so, rn, c), V(so, rn, c + 1),
+                                       V(s, rn, c - 1),  V(s, rn, c),  V(s, rn, c + 1),
+                                       V(s, r, cn),      V(s, rp, cn),
+                                       V(si, rn, c - 1), V(si, rn, c), V(si, rn, c + 1),
+                                       V(si, rp, cn),    V(si, r, cn)};
                 ok = true;
 #pragma unroll
-                for (int t = 0; t < 19; t++) ok = ok && !(best < nb[t]);
+                for (int t = 0; t < 19; t++) {
+                    nb[t] = nbv[t];
+                    ok = ok && !(best < nbv[t]);
+                }
             }
             const unsigned long long mo = __ballot(ok);
             if (ok) {
@@ -1757,6 +1793,40 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
                                                                        __builtin_amdgcn_mbcnt_lo((unsigned)mo, 0u));
                 rkey[slot] = ((uint32_t)o << 29) | ((uint32_t)z << 28) | ((uint32_t)y << 14) | (uint32_t)xx;
                 rsrc_[slot] = ((uint32_t)s << 28) | ((uint32_t)r << 14) | (uint32_t)c;
+                if (slot < kCubeCap && scan_cube) {
+                    // the 19 values fitQuadrat's first pass reads (fit_quad),
+                    // from the test's registers: k_nms_fit then gathers
+                    // nothing for a survivor that does not move
+                    // plus the six block values it needs (the block's opposite
+                    // corner is not read); loading them for every candidate
+                    // with the neighbours was slower (0.98 vs 0.92 ms scan)
+                    const int si = s - ds, rp = r - dr;
+                    const float b_r_cm = V(s, r, c - dc), b_rp_c = V(s, rp, c), b_rp_cm = V(s, rp, c - dc);
+                    const float i_r_c = V(si, r, c), i_r_cm = V(si, r, c - dc), i_rp_c = V(si, rp, c);
+                    // V(s + a, r + b, c + e) for the positions fit_quad reads
+                    auto so_at = [&](int b, int e) -> float {
+                        return b == 0 ? nb[4 + e] : (b == dr ? nb[7 + e] : nb[1 + e]);
+                    };
+                    auto s_at = [&](int b, int e) -> float {
+                        if (b == 0) return e == 0 ? best : (e == dc ? nb[12] : b_r_cm);
+                        if (b == dr) return nb[10 + e];
+                        return e == 0 ? b_rp_c : (e == dc ? nb[13] : b_rp_cm);
+                    };
+                    auto si_at = [&](int b, int e) -> float {       // no corner is read
+                        if (b == 0) return e == 0 ? i_r_c : (e == dc ? nb[18] : i_r_cm);
+                        if (b == dr) return nb[15 + e];
+                        return i_rp_c;
+                    };
+                    auto at = [&](int a, int b, int e) -> float {
+                        return a == 0 ? s_at(b, e) : (a == ds ? so_at(b, e) : si_at(b, e));
+                    };
+                    float4* dst = reinterpret_cast<float4*>(rcube + (size_t)slot * kCubeF);
+                    dst[0] = make_float4(best, at(1, 0, 0), at(-1, 0, 0), at(0, 1, 0));
+                    dst[1] = make_float4(at(0, -1, 0), at(0, 0, 1), at(0, 0, -1), at(1, 1, 0));
+                    dst[2] = make_float4(at(1, -1, 0), at(-1, 1, 0), at(-1, -1, 0), at(1, 0, 1));
+                    dst[3] = make_float4(at(1, 0, -1), at(-1, 0, 1), at(-1, 0, -1), at(0, 1, 1));
+                    dst[4] = make_float4(at(0, 1, -1), at(0, -1, 1), at(0, -1, -1), 0.f);
+                }
             }
             nsurv += (int)__popcll(mo);
         }
@@ -1768,14 +1838,16 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
 __global__ __launch_bounds__(256) void k_nms_scan(const float* __restrict__ resp, FrameParams P,
                                                   const OctaveParams* __restrict__ oct, LaunchPlan plan,
                                                   uint32_t* __restrict__ scan_key, uint32_t* __restrict__ scan_src,
-                                                  int* __restrict__ item_count, int nframes)
+                                                  float* __restrict__ scan_cube, int* __restrict__ item_count,
+                                                  int nframes)
 {
     __shared__ float sbest[4][64 * 4];                // one pass's candidates per wave
     __shared__ uint32_t sinfo[4][64 * 4];
     int f, gb;
     if (!xcd_frame_block(plan.nms_start[kMaxOct], nframes, f, gb)) return;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    nms_scan_item(resp, P, oct, plan, scan_key, scan_src, item_count, plan.nms_start[kMaxOct], f, gb, wv, sbest[wv],
+    nms_scan_item(resp, P, oct, plan, scan_key, scan_src, scan_cube, item_count, plan.nms_start[kMaxOct], f, gb, wv,
+                  sbest[wv],
                   sinfo[wv]);
 }
 
@@ -1835,7 +1907,13 @@ static void launch_excl_scan(const int* in, int n, int* out, int* bsum, hipStrea
     k_scan_add<<<nb, 256, 0, s>>>(out, n, bsum);
 }
 
-constexpr int kFitGrid = 1024;
+// k_nms_fit's grid: 5 waves per SIMD fit (90 VGPRs) = 1,280 workgroups of 4
+// waves; SURFHIP_FIT_GRID overrides (A/B)
+static int fit_grid()
+{
+    static const int g = getenv("SURFHIP_FIT_GRID") ? std::max(64, atoi(getenv("SURFHIP_FIT_GRID"))) : 1280;
+    return g;
+}
 
 // Pass 2: interpolation + makePoint, one lane per survivor of the whole batch
 // (grid-stride over the prefix of the scan items' survivor counts), so no
@@ -1845,12 +1923,13 @@ __global__ __launch_bounds__(256) void k_nms_fit(const int32_t* __restrict__ ii,
                                                  FrameParams P, const OctaveParams* __restrict__ oct,
                                                  const uint32_t* __restrict__ scan_key,
                                                  const uint32_t* __restrict__ scan_src,
+                                                 const float* __restrict__ scan_cube,
                                                  const int* __restrict__ soff, int nitems, int items_per_frame,
                                                  surfhip_point* __restrict__ cand, uint32_t* __restrict__ keys,
                                                  int* __restrict__ cand_count, int cap)
 {
     const int total = soff[nitems];
-    const int stride = kFitGrid * 256;
+    const int stride = (int)gridDim.x * 256;
     for (int base = blockIdx.x * 256 + (threadIdx.x & ~63); base < total; base += stride) {
         const int t = base + (int)lane_id();
         const bool act = t < total;
@@ -1865,14 +1944,22 @@ __global__ __launch_bounds__(256) void k_nms_fit(const int32_t* __restrict__ ii,
                 if (soff[mid] <= t) lo = mid; else hi = mid;
             }
             f = lo / items_per_frame;
-            const size_t src_i = (size_t)lo * kItemCap + (t - soff[lo]);
+            const int idx = t - soff[lo];                // survivor index within its scan item
+            const size_t src_i = (size_t)lo * kItemCap + idx;
             key = scan_key[src_i];
             const uint32_t src = scan_src[src_i];
             const int o = (int)(key >> 29);
             const OctaveParams& q = oct[o];
             const OctView V = make_view(resp + (size_t)f * P.resp_stride, q, o);
             const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
-            ok = nms_fit_point(I, V, P, q, o, (int)(src >> 28), (int)((src >> 14) & 0x3fffu), (int)(src & 0x3fffu), pt);
+            const float4* cube = idx < kCubeCap && scan_cube
+                ? reinterpret_cast<const float4*>(scan_cube + ((size_t)lo * kCubeCap + idx) * kCubeF) : nullptr;
+#ifndef SURF_DIAG_NOFIT
+            ok = nms_fit_point(I, V, P, q, o, (int)(src >> 28), (int)((src >> 14) & 0x3fffu), (int)(src & 0x3fffu),
+                               cube, pt);
+#else
+            ok = (src & 1u) && I != nullptr && V.F != nullptr && cube != nullptr;
+#endif
         }
         // Survivor t of frame f goes to slot t - (f's first survivor): the
         // slots are the survivors' scan order, so which candidates a frame
@@ -1902,16 +1989,19 @@ __global__ __launch_bounds__(256) void k_nms_fit(const int32_t* __restrict__ ii,
 
 hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,
                       const OctaveParams* d_oct, const LaunchPlan& plan, uint32_t* scan_key, uint32_t* scan_src,
-                      int* item_count, int* item_off, surfhip_point* cand, uint32_t* keys, int* cand_count, int cap,
-                      hipStream_t s)
+                      float* scan_cube, int* item_count, int* item_off, surfhip_point* cand, uint32_t* keys,
+                      int* cand_count, int cap, hipStream_t s)
 {
     const int per = plan.nms_start[kMaxOct];
     if (per == 0) return hipSuccess;
-    k_nms_scan<<<dim3(frame_grid(nframes) * per), 256, 0, s>>>(resp, P, d_oct, plan, scan_key, scan_src, item_count,
-                                                                nframes);
+    static const bool no_cube = getenv("SURFHIP_FIT_CUBE") && atoi(getenv("SURFHIP_FIT_CUBE")) == 0;   // A/B
+    if (no_cube) scan_cube = nullptr;
+    k_nms_scan<<<dim3(frame_grid(nframes) * per), 256, 0, s>>>(resp, P, d_oct, plan, scan_key, scan_src, scan_cube,
+                                                                item_count, nframes);
     const int nitems = nframes * per * 4;
     launch_excl_scan(item_count, nitems, item_off, item_off + nitems + 1, s);
-    k_nms_fit<<<kFitGrid, 256, 0, s>>>(ii, resp, P, d_oct, scan_key, scan_src, item_off, nitems, per * 4, cand, keys,
+    k_nms_fit<<<fit_grid(), 256, 0, s>>>(ii, resp, P, d_oct, scan_key, scan_src, scan_cube, item_off, nitems, per * 4,
+                                         cand, keys,
                                        cand_count, cap);
     return hipGetLastError();
 }
@@ -3048,12 +3138,10 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
                     // so hipcc's outstanding-load count stays exact.
                     uint32_t X[8], Y[8], Z[8];
                     const int tb = t0 + hh;
-                    {
-                        const Raw q0 = ldraw(tb - 2), q1 = ldraw(tb);
-                        proc(q0, X);
-                        proc(q1, Y);
-                    }
+                    const Raw q0 = ldraw(tb - 2), q1 = ldraw(tb);
                     Raw s0 = ldraw(tb + 2), s1 = ldraw(tb + 4), s2 = ldraw(tb + 6);
+                    proc(q0, X);
+                    proc(q1, Y);
                     for (int n = 0; n < nmax; n += 3) {
                         const int t = tb + 2 * n;
                         proc(s0, Z);
@@ -3154,13 +3242,22 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
                             for (int e = 0; e < NS; e++) acc[R][e] = fmaf(S[e], wrr[R], acc[R][e]);
                     };
                     uint32_t X[8], Y[8], Z[8];
-                    {
-                        const Seg q0 = ldseg(pb - 2);
-                        proc(q0, X);
-                        const Seg q1 = ldseg(pb);
-                        proc(q1, Y);
-                    }
+                    // all five row loads in flight before the first LDS
+                    // staging (proc's fences would otherwise hold each load
+                    // back until the previous rows are staged: three memory
+                    // round trips per keypoint before the loop)
+#ifndef SURF_DIAG_DESC_SERIAL
+                    const Seg q0 = ldseg(pb - 2), q1 = ldseg(pb);
                     Seg s0 = ldseg(pb + 2), s1 = ldseg(pb + 4), s2 = ldseg(pb + 6);
+                    proc(q0, X);
+                    proc(q1, Y);
+#else
+                    const Seg q0 = ldseg(pb - 2);
+                    proc(q0, X);
+                    const Seg q1 = ldseg(pb);
+                    proc(q1, Y);
+                    Seg s0 = ldseg(pb + 2), s1 = ldseg(pb + 4), s2 = ldseg(pb + 6);
+#endif
 #ifdef SURF_DIAG_NOROWS
                     continue;
 #endif
