@@ -2071,28 +2071,35 @@ __global__ __launch_bounds__(1024) void k_sort(const surfhip_point* __restrict__
     // times (octave, layer, y); the band order sweeps it once, so the few
     // hundred keypoints an XCD describes at a time share their integral-image
     // rows in that XCD's L2.
+    // A counting sort by band: the order within a band is free (describe
+    // writes each descriptor at its canonical index; the order only groups
+    // the keypoints an XCD describes at a time), so two passes of LDS atomics
+    // replace round 2's second bitonic sort (78 barrier passes for 4,096 keys).
     int* ord = order + (size_t)f * max_pts;
-    int nb = 1;
-    while (nb < keep) nb <<= 1;
-    if (nb > 2 * kSortCap) {
-        for (int t = threadIdx.x; t < keep; t += blockDim.x) ord[t] = t;
-        return;
-    }
     __threadfence_block();
     __syncthreads();                          // s[] is dead, out[] is written
-    uint32_t* bk = reinterpret_cast<uint32_t*>(sk);
-    for (int t = threadIdx.x; t < nb; t += blockDim.x) {
-        uint32_t k = 0xffffffffu;
-        if (t < keep) {
-            const float y = out[(size_t)f * max_pts + t].y;
-            const uint32_t band = min((uint32_t)max(y, 0.f) >> 4, 4095u);
-            k = (band << 20) | (uint32_t)t;
-        }
-        bk[t] = k;
+    constexpr int NBAND = 4096;               // 16-row bands of frames up to 65,536 rows
+    uint32_t* bc = reinterpret_cast<uint32_t*>(sk);
+    __shared__ uint32_t wsum[32];
+    for (int b = threadIdx.x; b < NBAND; b += blockDim.x) bc[b] = 0u;
+    __syncthreads();
+    auto band_of = [&](int t) -> uint32_t {
+        const float y = out[(size_t)f * max_pts + t].y;
+        return min((uint32_t)max(y, 0.f) >> 4, (uint32_t)NBAND - 1u);
+    };
+    for (int t = threadIdx.x; t < keep; t += blockDim.x) atomicAdd(&bc[band_of(t)], 1u);
+    __syncthreads();
+    {
+        constexpr int PER = NBAND / 1024;     // blockDim.x == 1024
+        uint32_t v[PER];
+#pragma unroll
+        for (int k = 0; k < PER; k++) v[k] = bc[PER * threadIdx.x + k];
+        block_excl_scan<PER>(v, wsum);
+#pragma unroll
+        for (int k = 0; k < PER; k++) bc[PER * threadIdx.x + k] = v[k];
     }
     __syncthreads();
-    bitonic_sort(bk, nb);
-    for (int t = threadIdx.x; t < keep; t += blockDim.x) ord[t] = (int)(bk[t] & 0xfffffu);
+    for (int t = threadIdx.x; t < keep; t += blockDim.x) ord[atomicAdd(&bc[band_of(t)], 1u)] = t;
 }
 
 // Small batches (nframes <= kRankBatch): the canonical order by ranks,
