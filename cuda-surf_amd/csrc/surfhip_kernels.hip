@@ -2031,6 +2031,31 @@ __device__ void bitonic_sort(PtrT s, int n)
     }
 }
 
+// The same network on an LDS array with 1024 threads: pair p of pass (k, j)
+// is elements (i, i + j), i = 2p - (p mod j), so every thread works every
+// pass, and a wave's 64 pairs (p = 64 w .. 64 w + 63 + 1024 m) cover the
+// 128-element blocks [128 (w + 16 m), +128) whenever j <= 64: those passes
+// need only a wave-level sync; a block barrier is kept around every pass
+// with j >= 128 (63 of the 78 passes of a 4,096-key sort skip it).
+__device__ void bitonic_sort_lds(uint64_t* s, int n)
+{
+    const int npairs = n >> 1;
+    for (int k = 2; k <= n; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int p = threadIdx.x; p < npairs; p += 1024) {
+                const int i = 2 * p - (p & (j - 1));
+                const uint64_t a = s[i], b = s[i + j];
+                const bool up = (i & k) == 0;
+                if ((a > b) == up) { s[i] = b; s[i + j] = a; }
+            }
+            const int nj = j > 1 ? j >> 1 : k;          // the next pass's distance
+            if (j >= 128 || (nj >= 128 && k < n)) __syncthreads();
+            else wave_sync();
+        }
+    }
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(1024) void k_sort(const surfhip_point* __restrict__ cand,
                                                const uint32_t* __restrict__ keys,
                                                uint64_t* __restrict__ gscratch, const int* __restrict__ cand_count,
@@ -2057,7 +2082,8 @@ __global__ __launch_bounds__(1024) void k_sort(const surfhip_point* __restrict__
     }
     if (mine) atomicAdd(&nvalid, mine);
     __syncthreads();
-    bitonic_sort(s, n);
+    if (in_lds && blockDim.x == 1024) bitonic_sort_lds(s, n);
+    else bitonic_sort(s, n);
     const int valid = nvalid;
     // accepted candidates beyond the cap were dropped: report it
     if (threadIdx.x == 0 && cand_count[f] > valid) atomicOr(status, 1);
