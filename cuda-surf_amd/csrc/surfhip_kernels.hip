@@ -1759,11 +1759,13 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
             const int ci = c0 + (int)lane_id();
             bool ok = false;
             int s = 0, r = 0, c = 0, xx = 0, y = 0, ds = 1, dr = 1, dc = 1;
+            int u = 0, cas = 0, srcl = (int)lane_id();
             float best = 0.f, nb[19];
             if (ci < ncand) {
                 best = sbest[ci];
                 const uint32_t info = sinfo[ci];
-                const int u = (int)(info >> 9), cas = (int)((info >> 6) & 7u);
+                u = (int)(info >> 9); cas = (int)((info >> 6) & 7u);
+                srcl = (int)(info & 63u);
                 xx = bx0 + (int)(info & 63u);
                 y = y0 + 4 * u;
                 const int i = mb + y * 2, jx = mb + xx * 2;
@@ -1788,6 +1790,20 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
                 }
             }
             const unsigned long long mo = __ballot(ok);
+            // the survivors' 2x2x2 blocks from the lanes that loaded them
+            // (their registers vc, this pass): 32 cross-lane reads with the
+            // whole wave active, each lane keeping its block row u's 8
+            float blk[8];
+            if (mo && scan_cube) {
+#pragma unroll
+                for (int uu = 0; uu < NU; uu++)
+#pragma unroll
+                    for (int t = 0; t < 8; t++) {
+                        const float g = __shfl(vc[uu][t], srcl, 64);
+                        if (uu == 0) blk[t] = g;
+                        else blk[t] = u == uu ? g : blk[t];
+                    }
+            }
             if (ok) {
                 const int slot = nsurv + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mo >> 32),
                                                                        __builtin_amdgcn_mbcnt_lo((unsigned)mo, 0u));
@@ -1798,11 +1814,16 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
                     // from the test's registers: k_nms_fit then gathers
                     // nothing for a survivor that does not move
                     // plus the six block values it needs (the block's opposite
-                    // corner is not read); loading them for every candidate
-                    // with the neighbours was slower (0.98 vs 0.92 ms scan)
-                    const int si = s - ds, rp = r - dr;
-                    const float b_r_cm = V(s, r, c - dc), b_rp_c = V(s, rp, c), b_rp_cm = V(s, rp, c - dc);
-                    const float i_r_c = V(si, r, c), i_r_cm = V(si, r, c - dc), i_rp_c = V(si, rp, c);
+                    // corner is not read): block index cas ^ {col, row, scale}
+                    // bits (loading them from memory cost the scan a round trip)
+                    auto bsel = [&](int x) -> float {
+                        float v = blk[0];
+#pragma unroll
+                        for (int t = 1; t < 8; t++) v = x == t ? blk[t] : v;
+                        return v;
+                    };
+                    const float b_r_cm = bsel(cas ^ 1), b_rp_c = bsel(cas ^ 2), b_rp_cm = bsel(cas ^ 3);
+                    const float i_r_c = bsel(cas ^ 4), i_r_cm = bsel(cas ^ 5), i_rp_c = bsel(cas ^ 6);
                     // V(s + a, r + b, c + e) for the positions fit_quad reads
                     auto so_at = [&](int b, int e) -> float {
                         return b == 0 ? nb[4 + e] : (b == dr ? nb[7 + e] : nb[1 + e]);
