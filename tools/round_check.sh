@@ -12,3 +12,5 @@ tail -2 gpurun_out/rc_${TAG}_pytest.log
 timeout -k 10 300 python -u bench.py > gpurun_out/rc_${TAG}_bench.json 2> gpurun_out/rc_${TAG}_bench.err || { tail -20 gpurun_out/rc_${TAG}_bench.err; exit 1; }
 cat gpurun_out/rc_${TAG}_bench.json
 bash tools/profile_round.sh ${TAG}
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('SMOKE_OK')" > gpurun_out/rc_${TAG}_smoke.log 2>&1 || { tail -20 gpurun_out/rc_${TAG}_smoke.log; exit 1; }
+tail -1 gpurun_out/rc_${TAG}_smoke.log
