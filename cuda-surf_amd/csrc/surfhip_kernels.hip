@@ -1671,6 +1671,7 @@ __device__ __forceinline__ int wave_append(bool ok, int* counter)
 // One workgroup = 4 waves x (64 block columns x kScanRows/4 block rows) of
 // one (frame, octave, level), a wave's rows in passes of 4 whose loads are
 // issued one pass ahead; XCD x takes frames x, x + 8, ...
+template <bool CUBE>
 __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, const FrameParams& P,
                                               const OctaveParams* __restrict__ oct, const LaunchPlan& plan,
                                               uint32_t* __restrict__ scan_key, uint32_t* __restrict__ scan_src,
@@ -1794,7 +1795,7 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
             // (their registers vc, this pass): 32 cross-lane reads with the
             // whole wave active, each lane keeping its block row u's 8
             float blk[8];
-            if (mo && scan_cube) {
+            if (CUBE && mo) {
 #pragma unroll
                 for (int uu = 0; uu < NU; uu++)
 #pragma unroll
@@ -1809,7 +1810,7 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
                                                                        __builtin_amdgcn_mbcnt_lo((unsigned)mo, 0u));
                 rkey[slot] = ((uint32_t)o << 29) | ((uint32_t)z << 28) | ((uint32_t)y << 14) | (uint32_t)xx;
                 rsrc_[slot] = ((uint32_t)s << 28) | ((uint32_t)r << 14) | (uint32_t)c;
-                if (slot < kCubeCap && scan_cube) {
+                if (CUBE && slot < kCubeCap) {
                     // the 19 values fitQuadrat's first pass reads (fit_quad),
                     // from the test's registers: k_nms_fit then gathers
                     // nothing for a survivor that does not move
@@ -1856,6 +1857,10 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
     if (lane_id() == 0u && nsurv > 0) item_count[item] = nsurv;
 }
 
+// CUBE: write the survivors' fit records (k_nms_fit's first pass then reads
+// no planes); without it the scan keeps 38 instead of 76 VGPRs, which single
+// frames (config #2: a few hundred survivors) prefer
+template <bool CUBE>
 __global__ __launch_bounds__(256) void k_nms_scan(const float* __restrict__ resp, FrameParams P,
                                                   const OctaveParams* __restrict__ oct, LaunchPlan plan,
                                                   uint32_t* __restrict__ scan_key, uint32_t* __restrict__ scan_src,
@@ -1867,7 +1872,7 @@ __global__ __launch_bounds__(256) void k_nms_scan(const float* __restrict__ resp
     int f, gb;
     if (!xcd_frame_block(plan.nms_start[kMaxOct], nframes, f, gb)) return;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    nms_scan_item(resp, P, oct, plan, scan_key, scan_src, scan_cube, item_count, plan.nms_start[kMaxOct], f, gb, wv,
+    nms_scan_item<CUBE>(resp, P, oct, plan, scan_key, scan_src, scan_cube, item_count, plan.nms_start[kMaxOct], f, gb, wv,
                   sbest[wv],
                   sinfo[wv]);
 }
@@ -2015,9 +2020,11 @@ hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const F
 {
     const int per = plan.nms_start[kMaxOct];
     if (per == 0) return hipSuccess;
-    static const bool no_cube = getenv("SURFHIP_FIT_CUBE") && atoi(getenv("SURFHIP_FIT_CUBE")) == 0;   // A/B
-    if (no_cube) scan_cube = nullptr;
-    k_nms_scan<<<dim3(frame_grid(nframes) * per), 256, 0, s>>>(resp, P, d_oct, plan, scan_key, scan_src, scan_cube,
+    static const char* ce = getenv("SURFHIP_FIT_CUBE");                  // A/B: 0 off, 1 on
+    const bool cube = ce ? atoi(ce) != 0 : nframes > kGatherBatch;
+    if (!cube) scan_cube = nullptr;
+    auto* scan = cube ? &k_nms_scan<true> : &k_nms_scan<false>;
+    scan<<<dim3(frame_grid(nframes) * per), 256, 0, s>>>(resp, P, d_oct, plan, scan_key, scan_src, scan_cube,
                                                                 item_count, nframes);
     const int nitems = nframes * per * 4;
     launch_excl_scan(item_count, nitems, item_off, item_off + nitems + 1, s);

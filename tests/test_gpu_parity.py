@@ -199,6 +199,23 @@ def test_detect_describe_synthetic(surf, orc, upright, extend):
         compare_frame(res["pts"][f], res["desc"][f], o_pts, o_desc, upright)
 
 
+@pytest.mark.parametrize("cube", ["0", "1"])
+def test_fit_records_from_scan(surf, orc, monkeypatch, cube):
+    """k_nms_fit's first pass from the scan's record of the 19 responses
+    (SURFHIP_FIT_CUBE=1, the default for batches > 8) or from the planes
+    (=0, the small-batch default): the same keypoints, bit for bit."""
+    monkeypatch.setenv("SURFHIP_FIT_CUBE", cube)
+    w, h = 640, 480
+    frames = surf.synth_frames(3, w, h, first=300)
+    param = surf.make_param(4, 4.0, upright=True)
+    res = gpu_run(surf, param, frames, w, h)
+    op = orc.make_param(4, 4.0, upright=True)
+    for f in range(3):
+        o_pts, o_desc, nc = orc.detect(op, frames[f], w, h)
+        assert res["cand"][f] == nc
+        compare_frame(res["pts"][f], res["desc"][f], o_pts, o_desc, True)
+
+
 @pytest.mark.parametrize("extend", [False, True])
 @pytest.mark.parametrize("atomic", [False, True])
 def test_rotated_descriptor_kernels(surf, orc, monkeypatch, extend, atomic):
