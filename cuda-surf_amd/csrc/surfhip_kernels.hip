@@ -1677,7 +1677,7 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
                                               uint32_t* __restrict__ scan_key, uint32_t* __restrict__ scan_src,
                                               float* __restrict__ scan_cube,
                                               int* __restrict__ item_count, int nitems_frame, int f, int gb, int wv,
-                                              float* sbest, uint32_t* sinfo)
+                                              float* sbest, uint32_t* sinfo, float* sblk)
 {
     constexpr int NU = 4;                    // block rows per lane per pass
     constexpr int NIT = kScanRows / 4 / NU;  // passes: the next pass's loads are issued first
@@ -1751,6 +1751,12 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
                                                                        __builtin_amdgcn_mbcnt_lo((unsigned)m[u], 0u));
                 sbest[slot] = bst[u];
                 sinfo[slot] = ((uint32_t)u << 9) | ((uint32_t)cs[u] << 6) | lane_id();
+                // the block's 8 values for the fit record (first 64 candidates)
+                if (CUBE && slot < 64) {
+                    float4* bd = reinterpret_cast<float4*>(sblk + 8 * slot);
+                    bd[0] = make_float4(vc[u][0], vc[u][1], vc[u][2], vc[u][3]);
+                    bd[1] = make_float4(vc[u][4], vc[u][5], vc[u][6], vc[u][7]);
+                }
             }
             ncand += (int)__popcll(m[u]);
         }
@@ -1760,13 +1766,12 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
             const int ci = c0 + (int)lane_id();
             bool ok = false;
             int s = 0, r = 0, c = 0, xx = 0, y = 0, ds = 1, dr = 1, dc = 1;
-            int u = 0, cas = 0, srcl = (int)lane_id();
+            int u = 0, cas = 0;
             float best = 0.f, nb[19];
             if (ci < ncand) {
                 best = sbest[ci];
                 const uint32_t info = sinfo[ci];
                 u = (int)(info >> 9); cas = (int)((info >> 6) & 7u);
-                srcl = (int)(info & 63u);
                 xx = bx0 + (int)(info & 63u);
                 y = y0 + 4 * u;
                 const int i = mb + y * 2, jx = mb + xx * 2;
@@ -1791,20 +1796,6 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
                 }
             }
             const unsigned long long mo = __ballot(ok);
-            // the survivors' 2x2x2 blocks from the lanes that loaded them
-            // (their registers vc, this pass): 32 cross-lane reads with the
-            // whole wave active, each lane keeping its block row u's 8
-            float blk[8];
-            if (CUBE && mo) {
-#pragma unroll
-                for (int uu = 0; uu < NU; uu++)
-#pragma unroll
-                    for (int t = 0; t < 8; t++) {
-                        const float g = __shfl(vc[uu][t], srcl, 64);
-                        if (uu == 0) blk[t] = g;
-                        else blk[t] = u == uu ? g : blk[t];
-                    }
-            }
             if (ok) {
                 const int slot = nsurv + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mo >> 32),
                                                                        __builtin_amdgcn_mbcnt_lo((unsigned)mo, 0u));
@@ -1813,18 +1804,24 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
                 if (CUBE && slot < kCubeCap) {
                     // the 19 values fitQuadrat's first pass reads (fit_quad),
                     // from the test's registers: k_nms_fit then gathers
-                    // nothing for a survivor that does not move
-                    // plus the six block values it needs (the block's opposite
-                    // corner is not read): block index cas ^ {col, row, scale}
-                    // bits (loading them from memory cost the scan a round trip)
-                    auto bsel = [&](int x) -> float {
-                        float v = blk[0];
-#pragma unroll
-                        for (int t = 1; t < 8; t++) v = x == t ? blk[t] : v;
-                        return v;
-                    };
-                    const float b_r_cm = bsel(cas ^ 1), b_rp_c = bsel(cas ^ 2), b_rp_cm = bsel(cas ^ 3);
-                    const float i_r_c = bsel(cas ^ 4), i_r_cm = bsel(cas ^ 5), i_rp_c = bsel(cas ^ 6);
+                    // nothing for a survivor that does not move; plus the six
+                    // block values it needs (the block's opposite corner is
+                    // not read), block index cas ^ {col, row, scale} bits, from
+                    // the block the candidate's lane staged in LDS at
+                    // compaction (a memory reload cost the scan a round trip,
+                    // cross-lane reads kept the block registers live: 76 VGPRs)
+                    // (a candidate past the first 64 of its pass reloads them:
+                    // the fit reads a record for every survivor slot < kCubeCap)
+                    float b_r_cm, b_rp_c, b_rp_cm, i_r_c, i_r_cm, i_rp_c;
+                    if (ci < 64) {
+                        const float* bs = sblk + 8 * ci;
+                        b_r_cm = bs[cas ^ 1]; b_rp_c = bs[cas ^ 2]; b_rp_cm = bs[cas ^ 3];
+                        i_r_c = bs[cas ^ 4]; i_r_cm = bs[cas ^ 5]; i_rp_c = bs[cas ^ 6];
+                    } else {
+                        const int si = s - ds, rp = r - dr;
+                        b_r_cm = V(s, r, c - dc); b_rp_c = V(s, rp, c); b_rp_cm = V(s, rp, c - dc);
+                        i_r_c = V(si, r, c); i_r_cm = V(si, r, c - dc); i_rp_c = V(si, rp, c);
+                    }
                     // V(s + a, r + b, c + e) for the positions fit_quad reads
                     auto so_at = [&](int b, int e) -> float {
                         return b == 0 ? nb[4 + e] : (b == dr ? nb[7 + e] : nb[1 + e]);
@@ -1868,13 +1865,14 @@ __global__ __launch_bounds__(256) void k_nms_scan(const float* __restrict__ resp
                                                   int nframes)
 {
     __shared__ float sbest[4][64 * 4];                // one pass's candidates per wave
+    __shared__ __attribute__((aligned(16))) float sblk[4][64 * 8];   // blocks of its first 64 (CUBE)
     __shared__ uint32_t sinfo[4][64 * 4];
     int f, gb;
     if (!xcd_frame_block(plan.nms_start[kMaxOct], nframes, f, gb)) return;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     nms_scan_item<CUBE>(resp, P, oct, plan, scan_key, scan_src, scan_cube, item_count, plan.nms_start[kMaxOct], f, gb, wv,
                   sbest[wv],
-                  sinfo[wv]);
+                  sinfo[wv], sblk[wv]);
 }
 
 // Exclusive prefix of n ints (n up to ~2M): each workgroup scans 2048
