@@ -1288,7 +1288,8 @@ __global__ __launch_bounds__(farc::THREADS) void k_hess_far(const int32_t* __res
 #ifndef SURF_DIAG_FAR_NOACC
             far_bal<H, PL, ROWW, ST>(nfar, sidx, wv, ring, lane, acc + F.oc[0].accoff + lane,
                                      acc + F.oc[1].accoff + lane, acc + F.oc[2].accoff + lane, Y0 >> 3, Y0 >> 4,
-                                     Y0 >> 5, sh2, sh3, sh4);
+                                     Y0 >> 5, sh2, sh3, sh4, (int)((unsigned)(Y0 >> 3) % farc::NA),
+                                     (int)((unsigned)(Y0 >> 4) % farc::NA), (int)((unsigned)(Y0 >> 5) % farc::NA));
 #endif
         }
         __syncthreads();

@@ -83,7 +83,8 @@ def emit_balanced(R):
     wave-per-row split waited on the busiest row); each wave reads its items'
     rows from the ring and adds into the LDS accumulators (ds_add, so waves
     may share one).  Sample row of an item: i + k with i = Y0 / d (floor) and
-    k = ((R ph) mod d + j - dr) / d; accumulator row (i + k) mod NA."""
+    k = ((R ph) mod d + j - dr) / d; accumulator row (i + k) mod NA, from
+    b = i mod NA computed once per step (far_wrap)."""
     nw = R
     out = ["", f"// ---- load-balanced per-wave programs, {R} rows per step (see emit_balanced)"]
     for nfar in (1, 2, 3):
@@ -113,7 +114,7 @@ def emit_balanced(R):
                 out.append("template <int H, int PL, int ROWW, int ST>")
                 out.append(f"__device__ __forceinline__ void far_bal_n{nfar}_p{ph}_w{w}(const uint32_t* __restrict__ ring, "
                            "int lane, int* __restrict__ a0, int* __restrict__ a1, int* __restrict__ a2, int i0, int i1, "
-                           "int i2, int s0, int s1, int s2)")
+                           "int i2, int s0, int s1, int s2, int b0, int b1, int b2)")
                 out.append("{")
                 for oi in range(nfar):
                     mine = [it for it in bins[w] if it[1] == oi]
@@ -140,7 +141,7 @@ def emit_balanced(R):
                         out.append(f"        const uint32_t t{n} = {expr};")
                     for n, (_, _, _, j, k, dr, slot, cs) in enumerate(mine):
                         out.append(f"        if ((unsigned)(i{oi} + ({k})) < (unsigned)s{oi})")
-                        out.append(f"            atomicAdd(a{oi} + (((unsigned)(i{oi} + ({k})) % farc::NA) * 9 + {slot}) * "
+                        out.append(f"            atomicAdd(a{oi} + (far_wrap<{k}>(b{oi}) * 9 + {slot}) * "
                                    f"(ST / {d}), (int)t{n});")
                     out.append("    }")
                 out.append("}")
@@ -148,7 +149,8 @@ def emit_balanced(R):
     # dispatcher: step index Y0 / R gives the phase
     out.append("template <int H, int PL, int ROWW, int ST>")
     out.append("__device__ __forceinline__ void far_bal(int nfar, int step, int w, const uint32_t* __restrict__ ring, "
-               "int lane, int* a0, int* a1, int* a2, int i0, int i1, int i2, int s0, int s1, int s2)")
+               "int lane, int* a0, int* a1, int* a2, int i0, int i1, int i2, int s0, int s1, int s2, int b0, int b1, "
+               "int b2)")
     out.append("{")
     out.append(f"    const int ph = step & ((nfar == 3 ? {max(1, 32 // R)} : nfar == 2 ? {max(1, 16 // R)} : 1) - 1);")
     out.append(f"    switch (((nfar - 1) * 4 + ph) * {nw} + w) {{")
@@ -157,7 +159,7 @@ def emit_balanced(R):
         for ph in range(max(1, dmax // R)):
             for w in range(nw):
                 out.append(f"    case {((nfar - 1) * 4 + ph) * nw + w}: far_bal_n{nfar}_p{ph}_w{w}<H, PL, ROWW, ST>(ring, lane, "
-                           "a0, a1, a2, i0, i1, i2, s0, s1, s2); break;")
+                           "a0, a1, a2, i0, i1, i2, s0, s1, s2, b0, b1, b2); break;")
     out.append("    default: break;")
     out.append("    }")
     out.append("}")
@@ -168,6 +170,16 @@ def emit_balanced(R):
 def emit():
     lines = ["// Generated by tools/gen_far.py -- do not edit.",
              "// Far-octave corner programs for k_hess_far (see the generator's docstring).",
+             "",
+             "// accumulator row (i + K) mod NA from b = i mod NA (the row index of a",
+             "// valid sample row i + K >= 0; |K| < NA): one conditional wrap",
+             "template <int K>",
+             "__device__ __forceinline__ int far_wrap(int b)",
+             "{",
+             "    const int t = b + K;",
+             "    if constexpr (K >= 0) return t >= farc::NA ? t - farc::NA : t;",
+             "    else return t < 0 ? t + farc::NA : t;",
+             "}",
              ""]
     for i, R in enumerate(RS):
         lines.append(("#if" if i == 0 else "#elif") + f" SURF_FAR_R == {R}")
