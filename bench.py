@@ -7,20 +7,29 @@ a batch of 256 synthetic 1920x1080 u8 frames per GPU, 4 octaves, 64-D upright
 descriptors, thresh=4, sampling 2, init mask 9 (main.cpp:187-204), resident
 in HBM before the timed region.  One step = the whole hot path over one batch:
 integral -> Hessian (all octaves) -> NMS + interpolation -> canonical sort ->
-descriptors.  With N > 1 GPUs (one process per GPU, torch.distributed over
-RCCL) each rank processes its own 256 frames (weak scaling, config #4 at
-N = 8) and the compacted SurfPoint + descriptor slab of every rank is
-all-gathered over xGMI through libsurfcomm's surfhip_allgather (SURVEY.md
-8e) into a per-rank capacity agreed once before the timed region; the gather
-of batch i overlaps the compute of batch i+1 on a comm stream.  The run fails
-(exit 3, no JSON) if any frame hit max_pts, the candidate capacity
-overflowed, or a slab exceeded its capacity.
+descriptors.
+
+Multi-GPU (config #4 at N = 8): one process per GPU.  Under
+torch.distributed.run the ranks come from RANK/LOCAL_RANK/WORLD_SIZE (which
+must equal --gpus); a plain `python bench.py --gpus N` starts the N rank
+processes itself before anything touches the GPU.  Each rank processes its
+own 256 frames (weak scaling) and the compacted result slab of every rank is
+all-gathered over xGMI through libsurfcomm's surfhip_allgather (RCCL, the
+C-ABI data path; --gather full = SurfPoints + descriptors, points = SurfPoints
+only, descriptors stay sharded) into a per-rank capacity agreed once before
+the timed region; the gather of batch i overlaps the compute of batch i+1 on
+a comm stream.  The control plane (barriers, the capacity agreement, the
+RCCL id broadcast, the max-over-ranks time) runs over a gloo group, so each
+process holds exactly one RCCL communicator.  The run fails (exit 3, no
+JSON) if any frame hit max_pts, the candidate capacity overflowed, or a slab
+exceeded its capacity.
 
 Rank 0 prints ONE JSON line (the driver's contract), with a `roofline` object
-for the Hessian kernel (HIP events on the detector's stream inside the timed
-region; algorithmic bytes = integral image read once + valid responses
-written) and a `cpu_baseline` object (the oracle/ CPU restatement on a
-bounded sample of the same frames, rank 0 at N = 1 only).
+for the Hessian stage (HIP events on the detector's stream; algorithmic
+bytes = integral image read once + valid responses written), an `exchange`
+object (all-gather bytes and time per step; at N = 1 a 1-rank RCCL
+all-gather of the real slab) and a `cpu_baseline` object (the oracle/ CPU
+restatement on a bounded sample of the same frames, rank 0 at N = 1 only).
 """
 from __future__ import annotations
 
@@ -28,6 +37,8 @@ import argparse
 import importlib.util
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -48,14 +59,102 @@ def load_surf():
     return mod
 
 
+# ----------------------------------------------------------- rank launcher
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args) -> int | None:
+    """`--gpus N` without a launcher: start N rank processes (fresh
+    interpreters, so no process that touched the GPU ever execs) and return
+    the job's exit code; None when this process is itself a rank.  Runs
+    before torch is imported."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={env_world}", file=sys.stderr,
+                  flush=True)
+            sys.exit(2)
+        return None
+    if args.gpus <= 1:
+        return None
+    n = args.gpus
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc, live, kill_at = 0, list(procs), None
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 128 - r
+                for q in live:                     # a lost rank would leave the others in a collective
+                    q.terminate()
+                kill_at = time.time() + 20
+        if kill_at is not None and time.time() > kill_at:
+            for q in live:
+                q.kill()
+            kill_at = None
+        time.sleep(0.1)
+    return rc
+
+
+# ------------------------------------------------------------ CPU baseline
+
+def cpu_share() -> tuple[int, dict]:
+    """Threads for the CPU baseline: the CPUs this job may use (affinity,
+    capped by a cgroup CPU quota and by the job's OMP_NUM_THREADS share),
+    plus what the host has."""
+    host = os.cpu_count() or 1
+    try:
+        visible = len(os.sched_getaffinity(0))
+    except AttributeError:
+        visible = host
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    omp = int(omp) if omp and omp.isdigit() else None
+    share = visible
+    for lim in (quota, omp):
+        if lim:
+            share = min(share, lim)
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return share, {"host_cpus": host, "affinity_cpus": visible, "cgroup_cpu_quota": quota,
+                   "omp_num_threads": omp, "cpu_model": model}
+
+
 def cpu_baseline(frames, w, h, args):
     """The oracle (a scalar C restatement of the reference) on a bounded sample:
     passes over chunks of the same frames until about --cpu-seconds of wall
-    time, one frame per thread."""
+    time, one frame per thread, on every CPU this job may use."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # test infrastructure: the baseline only, never the measured path
     chunk = min(args.cpu_frames, frames.shape[0])
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    share, host = cpu_share()
+    threads = args.cpu_threads or share
     p = oracle.make_param(args.octaves, args.thresh, False, 9, 2, bool(args.upright), bool(args.extend), 4)
     secs, pts, n, start = 0.0, 0, 0, 0
     while secs < args.cpu_seconds or n == 0:
@@ -65,10 +164,13 @@ def cpu_baseline(frames, w, h, args):
         pts += k
         n += sub.shape[0]
         start = (start + chunk) % frames.shape[0]
-    return {"value": round(n / secs, 3), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n} frames ({chunk}-frame chunks cycling over the {frames.shape[0]} synthetic {w}x{h} "
-                      f"frames of the GPU batch), detect+describe, one frame per thread, {threads} threads, "
-                      f"{pts} keypoints, {secs:.2f} s wall"}
+    out = {"value": round(n / secs, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+           "sample": f"{n} frames ({chunk}-frame chunks cycling over the {frames.shape[0]} synthetic {w}x{h} "
+                     f"frames of the GPU batch), detect+describe, one frame per thread, {threads} threads "
+                     f"(the job's CPU share), {pts} keypoints, {secs:.2f} s wall; the herbertbay CPU SURF "
+                     f"named by BASELINE is not available offline, the oracle port stands in for it"}
+    out.update(host)
+    return out
 
 
 def pmc_traffic(args):
@@ -89,6 +191,19 @@ def pmc_traffic(args):
     return None, None
 
 
+def config_name(args, world) -> str:
+    """BASELINE.json config this run is (configs[1..4] = #2..#5)."""
+    hd = (args.width, args.height) == (1920, 1080) and args.octaves == 4 and args.upright and not args.extend
+    if hd and args.batch == 1 and world == 1:
+        return "config#2"
+    if hd and args.batch == 256:
+        return "config#4" if world == 8 else ("config#3" if world == 1 else f"config#3/#4 at {world} GPUs")
+    if ((args.width, args.height) == (3840, 2160) and args.octaves == 5 and not args.upright and args.extend
+            and args.batch == 64):
+        return "config#5" if world == 8 else f"config#5 per-rank shard at {world} GPU(s)"
+    return "custom"
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -106,8 +221,13 @@ def main():
     ap.add_argument("--exchange", choices=("rccl", "gloo"), default="rccl",
                     help="world > 1: slab all-gather through libsurfcomm (RCCL), or host-staged over gloo "
                          "(a rehearsal that runs several ranks on one GPU)")
+    ap.add_argument("--gather", choices=("full", "points"), default="full",
+                    help="world > 1: all-gather SurfPoints + descriptors, or SurfPoints only "
+                         "(descriptors stay on the rank that computed them)")
     ap.add_argument("--slab-headroom", type=float, default=1.10,
                     help="fixed per-rank slab capacity = max over ranks of the warm-up slab x this")
+    ap.add_argument("--no-exchange-probe", action="store_true",
+                    help="N = 1: skip the 1-rank RCCL all-gather of the real slab")
     ap.add_argument("--cpu-frames", type=int, default=128, help="frames per CPU baseline chunk")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline wall-time budget")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -121,7 +241,16 @@ def main():
     args = ap.parse_args()
     if args.max_pts <= 0:
         args.max_pts = 65536 if args.width * args.height <= 1920 * 1088 else 262144
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
 
+    rc = spawn_ranks(args)              # before torch: the launcher never touches the GPU
+    if rc is not None:
+        sys.exit(rc)
+    run_rank(args)
+
+
+def run_rank(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -129,17 +258,26 @@ def main():
     import torch
     import torch.distributed as dist
 
+    ndev = torch.cuda.device_count()
+    if world > 1 and args.exchange == "rccl" and ndev < world:
+        print(f"bench.py rank {rank}: --exchange rccl needs one GPU per rank ({world} ranks, {ndev} GPUs); "
+              f"--exchange gloo rehearses several ranks on one GPU", file=sys.stderr, flush=True)
+        sys.exit(2)
     # one process per GPU; with --exchange gloo several ranks may share a GPU
-    gpu = local % max(1, torch.cuda.device_count()) if world > 1 else 0
+    gpu = local % max(1, ndev) if world > 1 else 0
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
     if world > 1:
-        if args.exchange == "gloo":
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=dev)
+        # control plane only (barriers, capacity agreement, id broadcast, max
+        # time): gloo on host tensors; the data path is libsurfcomm's RCCL
+        dist.init_process_group("gloo")
     surf = load_surf()
     surf.set_device(dev.index)
+
+    def allreduce_max(v, dtype=torch.int64):
+        t = torch.tensor([v], dtype=dtype)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t.item()
 
     W, H, B = args.width, args.height, args.batch
     pitch = surf.align_up(W, 128)
@@ -155,6 +293,7 @@ def main():
     d_pts = torch.empty(B * args.max_pts * 48, dtype=torch.uint8, device=dev)
     d_desc = torch.empty(B * args.max_pts * nf, dtype=torch.float32, device=dev)
     d_cnt = torch.zeros(B, dtype=torch.int32, device=dev)
+    d_cnt_max = torch.zeros(B, dtype=torch.int32, device=dev)     # max over every step's counts
     profile = not args.no_profile
     # the timed loop runs unprofiled (the detector then overlaps the integral
     # with the u8 Hessian kernels on a side stream); stage times come from a
@@ -169,25 +308,28 @@ def main():
         else:
             det.detect_batch(d_frames.data_ptr(), B, pitch, H * pitch, d_pts.data_ptr(), d_desc.data_ptr(),
                              d_cnt.data_ptr())
+            torch.maximum(d_cnt_max, d_cnt, out=d_cnt_max)
 
     if args.hessian_only:
         det.run_integral(d_frames.data_ptr(), B, pitch, H * pitch)
 
-    # multi-GPU exchange: every rank packs its compacted
-    # SurfPoint + descriptor slab straight into its own section of a gather
-    # buffer of a FIXED per-rank capacity (agreed once, below) and the
-    # sections are all-gathered through the C-ABI (libsurfcomm,
-    # surfhip_allgather over RCCL) on a comm stream: no host synchronisation
-    # per step; gather(i) overlaps compute(i+1), two buffers alternate.
+    # multi-GPU exchange: every rank packs its compacted slab
+    # straight into its own section of a gather buffer of a FIXED per-rank
+    # capacity (agreed once, below) and the sections are all-gathered through
+    # the C-ABI (libsurfcomm, surfhip_allgather over RCCL) on a comm stream: no
+    # host synchronisation per step; gather(i) overlaps compute(i+1), two
+    # buffers alternate.
     exchange = world > 1 and not args.hessian_only
+    desc_ptr_for_slab = d_desc.data_ptr() if args.gather == "full" else None
     comm = comm_stream = None
     cap = 0
     gathered, ev_packed, ev_gathered = [None, None], [None, None], [None, None]
+    ag_events = []                                      # (start, end) on the comm stream, timed steps
     if exchange:
         for i in range(args.warmup):                  # the detector's steady state sizes the slab
             run_batch()
-        used = det.slab_bytes(B, det.batch_total(B))
-        cap = surf.dist.agree_slab_size(dist, torch, used, dev)     # once, outside the timed region
+        used = det.slab_bytes(B, det.batch_total(B), desc=args.gather == "full")
+        cap = int(allreduce_max(used))                 # once, outside the timed region
         cap = surf.align_up(int(cap * args.slab_headroom) + 64, 256)
         for k in range(2):
             gathered[k] = torch.empty(world * cap, dtype=torch.uint8, device=dev)
@@ -198,20 +340,25 @@ def main():
             uid = torch.zeros(surf.COMM_ID_BYTES, dtype=torch.uint8)
             if rank == 0:
                 uid[:] = torch.frombuffer(bytearray(surf.comm_unique_id()), dtype=torch.uint8)
-            uid_d = uid.to(dev)
-            dist.broadcast(uid_d, 0)
-            comm = surf.Comm(world, rank, bytes(uid_d.cpu().numpy().tobytes()))
+            dist.broadcast(uid, 0)
+            comm = surf.Comm(world, rank, bytes(uid.numpy().tobytes()))
 
     nstep = 0                                          # buffer i & 1 across warmup and timed steps
+    timing = [False]
 
     def gather(i):
         k = i & 1
         mine = gathered[k].data_ptr() + rank * cap
         if i >= 2:
             stream.wait_event(ev_gathered[k])         # gather(i-2) has read this buffer
-        det.pack_slab_cap(d_pts.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(), B, mine, cap)
+        # pack before the next detect_batch reuses the detector's scratch and status
+        det.pack_slab_cap(d_pts.data_ptr(), desc_ptr_for_slab, d_cnt.data_ptr(), B, mine, cap)
         ev_packed[k].record(stream)
         comm_stream.wait_event(ev_packed[k])
+        ev = None
+        if timing[0]:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record(comm_stream)
         if comm is not None:
             comm.allgather(mine, cap, gathered[k].data_ptr(), comm_stream.cuda_stream)
         else:                                         # --exchange gloo: host-staged rehearsal
@@ -219,9 +366,12 @@ def main():
                 chunks = list(gathered[k].view(world, cap).cpu().unbind(0))
                 dist.all_gather(chunks, chunks[rank].clone())
                 gathered[k].copy_(torch.cat(chunks).to(dev))
+        if ev is not None:
+            ev[1].record(comm_stream)
+            ag_events.append(ev)
         ev_gathered[k].record(comm_stream)
 
-    def step(i):
+    def step():
         nonlocal nstep
         run_batch()
         if exchange:
@@ -229,34 +379,38 @@ def main():
         nstep += 1
 
     for i in range(args.warmup):
-        step(i)
+        step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
 
+    timing[0] = True
     t_start = time.perf_counter()
     for i in range(args.steps):
-        step(i)
+        step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
+    timing[0] = False
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = float(allreduce_max(elapsed, torch.float64))
 
-    # no truncation anywhere: a frame at max_pts, a candidate-capacity
-    # overflow or a slab beyond the agreed capacity invalidates the run
+    # no truncation anywhere: a frame at max_pts (max over every step's
+    # counts), a candidate-capacity overflow or a slab beyond the agreed
+    # capacity invalidates the run.  The truncation flag and the slab flags
+    # are read from the last step; every step processes the same frames, so
+    # they are the same in every step.
     counts = d_cnt.cpu().numpy()
+    counts_max = d_cnt_max.cpu().numpy()
     problems = []
     if not args.hessian_only:
         if det.truncated():
             problems.append("candidate capacity overflow (surfhip_detector_status)")
-        if (counts >= args.max_pts).any():
-            problems.append(f"{int((counts >= args.max_pts).sum())} frames reached max_pts {args.max_pts}")
+        if (counts_max >= args.max_pts).any():
+            problems.append(f"{int((counts_max >= args.max_pts).sum())} frames reached max_pts {args.max_pts}")
     exchanged = None
     if exchange:
         last = (nstep - 1) & 1
@@ -268,25 +422,38 @@ def main():
                 problems.append(f"rank {r} slab flags {fl}")
                 continue
             c, pts, desc = surf.parse_slab(g[r])
-            if len(c) != B or (desc is not None and desc.shape[1] != nf) or len(pts) != int(c.sum()):
+            want_nf = nf if args.gather == "full" else 0
+            got_nf = 0 if desc is None else desc.shape[1]
+            if len(c) != B or got_nf != want_nf or len(pts) != int(c.sum()):
                 problems.append(f"rank {r} slab malformed")
             totals.append(int(c.sum()))
         c0, _, _ = surf.parse_slab(g[rank])
         if not np.array_equal(c0, counts):
             problems.append(f"rank {rank}: gathered counts differ from detect_batch's")
-        exchanged = {"backend": args.exchange, "slab_cap_bytes": cap, "gathered_bytes_per_step": world * cap,
-                     "keypoints_gathered_per_step": sum(totals)}
+        ag_ms = [a.elapsed_time(b) for a, b in ag_events]
+        ag_mean = float(np.mean(ag_ms)) if ag_ms else None
+        if world > 1 and ag_mean is not None:
+            ag_mean = float(allreduce_max(ag_mean, torch.float64))
+        payload = int(sum(totals)) * (48 + (4 * nf if args.gather == "full" else 0))
+        exchanged = {"backend": args.exchange, "mode": args.gather, "slab_cap_bytes": cap,
+                     "gathered_bytes_per_step": world * cap,
+                     "received_bytes_per_rank_per_step": (world - 1) * cap,
+                     "payload_bytes_per_step": payload,
+                     "keypoints_gathered_per_step": sum(totals),
+                     "allgather_ms_per_step": None if ag_mean is None else round(ag_mean, 4),
+                     "allgather_busbw_GBps": (None if not ag_mean else
+                                              round((world - 1) * cap / (ag_mean * 1e-3) / 1e9, 1)),
+                     "overlap": "gather(i) on a comm stream beside compute(i+1)"}
     if world > 1:
-        bad = torch.tensor([len(problems)], dtype=torch.int64, device=dev)
-        dist.all_reduce(bad, op=dist.ReduceOp.MAX)
-        if int(bad.item()) and not problems:
+        bad = allreduce_max(len(problems))
+        if int(bad) and not problems:
             problems.append("another rank reported truncation")
     if problems:
         print(f"bench.py rank {rank}: INVALID RUN: " + "; ".join(problems), file=sys.stderr, flush=True)
         sys.exit(3)
     kp_per_batch = int(counts.sum())
     if world > 1:
-        kt = torch.tensor([kp_per_batch], dtype=torch.int64, device=dev)
+        kt = torch.tensor([kp_per_batch], dtype=torch.int64)
         dist.all_reduce(kt)
         kp_total_batch = int(kt.item())
     else:
@@ -316,6 +483,12 @@ def main():
     torch.cuda.synchronize(dev)
     hess_ms = ev0.elapsed_time(ev1) / args.steps
 
+    # N = 1: what this rank's exchange would move -- a 1-rank RCCL all-gather
+    # (libsurfcomm) of the real slab, both modes, after the timed region
+    probe = None
+    if world == 1 and not args.hessian_only and not args.no_exchange_probe:
+        probe = exchange_probe(surf, torch, det, dev, stream, d_pts, d_desc, d_cnt, B, nf)
+
     frames_total = world * B * args.steps
     value = frames_total / elapsed
     result = None
@@ -323,12 +496,7 @@ def main():
         hb = det.hessian_bytes_per_frame() * B
         achieved = hb / (hess_ms * 1e-3) / 1e9
         traffic, traffic_tag = pmc_traffic(args)
-        if (W, H) == (1920, 1080) and args.octaves == 4:
-            cfg_name = "config#3"
-        elif (W, H) == (3840, 2160) and args.octaves == 5 and not args.upright and args.extend:
-            cfg_name = "config#5"
-        else:
-            cfg_name = "custom"
+        cfg_name = config_name(args, world)
         result = {
             "metric": METRIC if (W, H) == (1920, 1080) else f"{W}x{H} frames/sec (detect+describe)",
             "value": round(value, 2),
@@ -342,9 +510,10 @@ def main():
             "vs_baseline": None,
             "dtype": "u8/i32/f32",
             "data": f"synthetic (seeded Gaussian-blob {W}x{H} frames, resident in HBM)",
-            "config": {"workload": f"{cfg_name} batch {B} x {W}x{H} per GPU, {args.octaves} octaves, "
+            "config": {"workload": f"{cfg_name}: batch {B} x {W}x{H} per GPU, {args.octaves} octaves, "
                                    f"{nf}-D {'upright' if args.upright else 'rotated'} descriptors, thresh {args.thresh}"
-                                   + (", RCCL all-gather of compacted SurfPoint+descriptor slabs" if world > 1 else ""),
+                                   + (f", RCCL all-gather of compacted SurfPoint{'+descriptor' if args.gather == 'full' else ''} slabs"
+                                      if world > 1 else ""),
                        "frames_per_gpu_per_step": B, "width": W, "height": H, "octaves": args.octaves,
                        "nfeatures": nf, "upright": bool(args.upright), "parallelism": f"frames sharded x{world}"},
             "keypoints_per_s": round(kp_total_batch * args.steps / elapsed, 1),
@@ -361,6 +530,8 @@ def main():
         }
         if exchanged is not None:
             result["exchange"] = exchanged
+        elif probe is not None:
+            result["exchange"] = probe
         if world == 1 and not args.no_cpu and not args.hessian_only:
             result["cpu_baseline"] = cpu_baseline(frames, W, H, args)
         else:
@@ -372,6 +543,45 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def exchange_probe(surf, torch, det, dev, stream, d_pts, d_desc, d_cnt, B, nf, reps=5):
+    """Time a 1-rank RCCL all-gather (libsurfcomm) of this batch's slab in
+    both modes.  With one rank RCCL copies the section locally, so this is
+    the launch + copy floor of the exchange, not an xGMI rate."""
+    out = {"backend": "rccl (1 rank)", "note": "N = 1: the exchange is not in the timed step; the slab this "
+           "rank would contribute, all-gathered by a 1-rank RCCL communicator after the timed region"}
+    try:
+        uid = surf.comm_unique_id()
+        comm = surf.Comm(1, 0, uid)
+    except Exception as e:            # the probe is informational; the bench line stands without it
+        out["error"] = str(e)[:200]
+        return out
+    try:
+        total = det.batch_total(B)
+        cs = torch.cuda.Stream(dev)
+        for mode in ("full", "points"):
+            used = det.slab_bytes(B, total, desc=mode == "full")
+            cap = surf.align_up(used + 64, 256)
+            send = torch.empty(cap, dtype=torch.uint8, device=dev)
+            recv = torch.empty(cap, dtype=torch.uint8, device=dev)
+            det.pack_slab_cap(d_pts.data_ptr(), d_desc.data_ptr() if mode == "full" else None, d_cnt.data_ptr(),
+                              B, send.data_ptr(), cap)
+            torch.cuda.synchronize(dev)
+            comm.allgather(send.data_ptr(), cap, recv.data_ptr(), cs.cuda_stream)     # warm
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(cs)
+            for _ in range(reps):
+                comm.allgather(send.data_ptr(), cap, recv.data_ptr(), cs.cuda_stream)
+            e1.record(cs)
+            torch.cuda.synchronize(dev)
+            ms = e0.elapsed_time(e1) / reps
+            ok = bool(torch.equal(send, recv))
+            out[mode] = {"slab_bytes": used, "allgather_ms": round(ms, 4), "bytes_equal": ok}
+        out["keypoints"] = total
+    finally:
+        comm.close()
+    return out
 
 
 if __name__ == "__main__":

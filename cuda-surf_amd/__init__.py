@@ -327,6 +327,9 @@ class Detector:
         n = _lib.surfhip_hessian_plan(self.h, buf, len(buf))
         if n < 0:
             check(n, "hessian_plan")
+        if n >= len(buf):                     # the plan text was cut: ask again with room for all of it
+            buf = C.create_string_buffer(n + 1)
+            check(min(0, _lib.surfhip_hessian_plan(self.h, buf, len(buf))), "hessian_plan")
         return buf.value.decode()
 
     def slab_bytes(self, nframes: int, total: int, desc: bool = True) -> int:

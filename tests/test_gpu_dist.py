@@ -171,6 +171,39 @@ def test_bench_world2_loop_gloo_rehearsal():
     assert ex["backend"] == "gloo" and ex["keypoints_gathered_per_step"] == d["keypoints_per_step"] > 0
 
 
+@pytest.mark.parametrize("gather", ["full", "points"])
+def test_bench_spawns_its_ranks(gather):
+    """`python bench.py --gpus 2` with no launcher starts its own two rank
+    processes (before touching the GPU) and prints ONE line with n_gpus 2 and
+    the exchange's bytes and time per step."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--exchange", "gloo", "--gather", gather,
+           "--batch", "8", "--steps", "4", "--warmup", "2", "--no-cpu"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=REPO, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, r.stdout
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["steps"] == 4
+    ex = d["exchange"]
+    assert ex["mode"] == gather and ex["keypoints_gathered_per_step"] == d["keypoints_per_step"] > 0
+    per_kp = 48 + (4 * 64 if gather == "full" else 0)
+    assert ex["payload_bytes_per_step"] == ex["keypoints_gathered_per_step"] * per_kp
+    assert ex["allgather_ms_per_step"] > 0 and ex["gathered_bytes_per_step"] == 2 * ex["slab_cap_bytes"]
+
+
+def test_bench_single_gpu_exchange_probe():
+    """N = 1: the line carries a 1-rank RCCL all-gather of the real slab."""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--batch", "8", "--steps", "3",
+                        "--warmup", "1", "--no-cpu"], capture_output=True, text=True, timeout=240, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    ex = d["exchange"]
+    assert "error" not in ex, ex
+    assert ex["full"]["bytes_equal"] and ex["points"]["bytes_equal"]
+    assert ex["full"]["slab_bytes"] > ex["points"]["slab_bytes"] > 0
+
+
 _UNDER_TORCH = r"""
 import importlib.util, sys
 import torch
