@@ -93,6 +93,8 @@ struct LaunchPlan {
     int o01;                        // q0 and q1 in one launch (k_hess_q01)
     int vfar_n;                     // octaves 2 .. 1 + vfar_n on k_hess_vfar (u8 vertical streaming)
     int o1_nbx;
+    int hw_n;                       // octaves 1 .. hw_n on k_hess_w (u8, shared strip integral); 0: off
+    int hw_nstrips, hw_nblk;        // its strips per frame and blocks of 4 integral rows
 };
 // Octaves >= 2 on the streaming-accumulation kernel (k_hess_far): per far
 // octave, the corner terms of every (scale, dxx/dyy/dxy) sum grouped by

@@ -710,6 +710,7 @@ __global__ __launch_bounds__(o0::THREADS, 4) void k_hess_o0(const int32_t* __res
 #include "surfhip_hess_vfar.inc"
 #include "surfhip_hess_q0.inc"
 #include "surfhip_hess_q1.inc"
+#include "surfhip_hess_w.inc"
 
 // ----------------------------------------------------------------------
 // Octave 1 (4 px between samples, lobes 15/19/23: corner offsets -34..35):
@@ -980,17 +981,41 @@ static bool vfar_ok(const FrameParams& P, const OctaveParams& q, int o)
     return true;
 }
 
+// Octaves 1 .. n of the default geometry (sampling 2, init mask 9: lobes
+// 15/19/23, 31/39/47, 63/79/95) on k_hess_w; returns n (2 or 3) or 0.
+static int hw_octaves(const FrameParams& P, const OctaveParams* oct)
+{
+    if (P.sampling != 2 || P.noct < 3) return 0;
+    int n = 0;
+    for (int o = 1; o <= 3 && o < P.noct; o++) {
+        const OctaveParams& q = oct[o];
+        bool ok = q.delta == (2 << o) && q.nscale == 3 && q.init_scale == 2;
+        for (int i = 0; ok && i < 3; i++) {
+            const int K = hw::kof(o, i);
+            ok = q.mask[i] == 2 * K + 1 && q.x2[i] == K && q.x3[i] == 2 * K && q.x4[i] == 3 * K;
+        }
+        if (!ok) break;
+        n = o;
+    }
+    return n >= 2 ? n : 0;
+}
+
 void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, FarPlan& far, int max_batch)
 {
     int hb = 0, nb = 0;
     const char* ge = getenv("SURFHIP_HESS_GATHER");
     const bool gather = ge ? atoi(ge) != 0 : max_batch <= kGatherBatch;
+    // octaves 1-3 on k_hess_w (default); SURFHIP_HESS_W=0 keeps k_hess_q1 + k_hess_far (A/B)
+    const char* we = getenv("SURFHIP_HESS_W");
+    plan.hw_n = (!gather && !(we && atoi(we) == 0)) ? hw_octaves(P, oct) : 0;
+    plan.hw_nstrips = (P.W + hw::ST - 1) / hw::ST;
+    plan.hw_nblk = ((P.H / 4 + 1 + hw::U - 1) / hw::U) * hw::U;
     // k_hess_vfar (u8, 0.45 + 0.76 ms/batch for octaves 2 / 3) loses to the
     // integral-image LDS kernel k_hess_far (1.03 ms for both) for now: opt-in
     const bool use_vfar = getenv("SURFHIP_FAR_V") != nullptr;
     plan.vfar_n = 0;
     for (int o = 2; use_vfar && o < P.noct && o < 4 && vfar_ok(P, oct[o], o); o++) plan.vfar_n = o - 1;
-    if (plan.vfar_n > 0 || gather) far = FarPlan{};
+    if (plan.vfar_n > 0 || gather || plan.hw_n > 0) far = FarPlan{};   // octaves > hw_n: k_hessian
     else make_far_plan(P, oct, far);
     if (gather) plan.vfar_n = 0;
     plan.o0_lds = !gather && P.noct > 0 && o0_lds_ok(P, oct[0]);
@@ -1001,7 +1026,7 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
     // selects k_hess_v0 (integer accumulators) as the A/B reference
     plan.o0_split = getenv("SURFHIP_V0_SPLIT") ? atoi(getenv("SURFHIP_V0_SPLIT")) : 44;
     plan.o0_vstrips = (oct[0].sw + 63) / 64;
-    plan.o1_lds = !gather && P.noct > 1 && o1_lds_ok(P, oct[1]);
+    plan.o1_lds = !gather && P.noct > 1 && o1_lds_ok(P, oct[1]) && plan.hw_n == 0;
     plan.o1_v = plan.o1_lds && getenv("SURFHIP_O1_RING") == nullptr;   // A/B switch back to k_hess_o1
     // octave-1 kernel: default k_hess_q1 (packed fp32); SURFHIP_Q1=0 selects k_hess_v1
     plan.o1_q = getenv("SURFHIP_Q1") ? atoi(getenv("SURFHIP_Q1")) != 0 : 1;
@@ -1016,7 +1041,8 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
             const OctaveParams& q = oct[o];
             plan.hess_nbx[o] = (q.sw + 63) / 64;
             const bool on_far = o >= 2 && o < 2 + (plan.vfar_n > 0 ? plan.vfar_n : far.nfar);
-            if (!(o == 0 && plan.o0_lds) && !(o == 1 && plan.o1_lds) && !on_far)
+            const bool on_w = o >= 1 && o <= plan.hw_n;
+            if (!(o == 0 && plan.o0_lds) && !(o == 1 && plan.o1_lds) && !on_far && !on_w)
                 hb += plan.hess_nbx[o] * ((q.sh + 3) / 4);
             plan.nms_nbx[o] = (q.nms_gx + 63) / 64;
             plan.nms_nby[o] = (q.nms_gy + kScanRows - 1) / kScanRows;
@@ -1051,6 +1077,7 @@ std::string hessian_plan_text(const LaunchPlan& plan, const FarPlan& far, const 
         if (plan.o1_v) add(plan.o1_q ? "k_hess_q1" : "k_hess_v1", 1, 1);
         else if (plan.o1_lds) add("k_hess_o1", 1, 1);
     }
+    if (plan.hw_n > 0) add("k_hess_w", 1, plan.hw_n);
     if (plan.vfar_n > 0) add("k_hess_vfar", 2, 1 + plan.vfar_n);
     if (far.nfar > 0) add("k_hess_far", far.oc[0].o, far.oc[far.nfar - 1].o);
     if (plan.hess_start[kMaxOct] > 0) {
@@ -1406,6 +1433,16 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
         }
     } else if (plan.o1_lds && iip)
         k_hess_o1<<<dim3(nf8 * plan.o1_nbx), o1::THREADS, 0, s>>>(ii, resp, P, h_oct[1], plan.o1_nbx, nframes);
+    if (plan.hw_n > 0 && frames && u8p) {
+        const dim3 g(nf8 * plan.hw_nstrips);
+        const OctaveParams& q3 = h_oct[plan.hw_n >= 3 ? 3 : 2];
+        if (plan.hw_n >= 3)
+            k_hess_w<3><<<g, hw::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[1], h_oct[2], q3,
+                                                  plan.hw_nstrips, nframes, plan.hw_nblk);
+        else
+            k_hess_w<2><<<g, hw::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[1], h_oct[2], q3,
+                                                  plan.hw_nstrips, nframes, plan.hw_nblk);
+    }
     if (plan.vfar_n > 0 && frames && u8p) {
         // octave 2: 3 vertical segments, octave 3: 2 (parallelism); one launch each
         for (int o = 2; o < 2 + plan.vfar_n; o++) {
