@@ -87,6 +87,7 @@ namespace surf
             det_w = whp0.x;
             det_h = whp0.y;
             det_pts = result.max_pts;
+            warned_trunc = false;
         }
         int n = 0;
         float* dptr = nullptr;
@@ -95,6 +96,20 @@ namespace surf
         result.num_pts = n;
         if (desc && desc_addr)
             *desc_addr = dptr;
+        // more NMS survivors than the detector's candidate capacity: the frame
+        // kept the first ones in scan order (deterministic, include/surfhip.h);
+        // the reference keeps an arbitrary subset and says nothing
+        // (surfd.cu:822-831) -- say it once per detector
+        int trunc = 0;
+        CHECK(surfhip_detector_status(det, &trunc));
+        if (trunc && !warned_trunc)
+        {
+            int cap = 0;
+            CHECK(surfhip_detector_capacity(det, &cap));
+            fprintf(stderr, "Surfor::detectAndCompute: a frame had more than %d scale-space maxima; the first %d "
+                            "in scan order were interpolated (raise max_pts to keep all)\n", cap, cap);
+            warned_trunc = true;
+        }
         // surf.cpp:335-342: the first 6 fields (7 with rotated descriptors)
         if (result.h_data != nullptr && n > 0)
         {

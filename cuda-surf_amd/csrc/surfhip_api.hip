@@ -271,8 +271,9 @@ int surfhip_make_param(surfhip_param* out, int noctaves, float thresh, int doubl
     out->mag_factor = 12 / desc_wsz;
     out->orient_size = 4 + (extend ? 4 : 0);
     out->nfeatures = desc_wsz * desc_wsz * out->orient_size;
-    // the NMS kernel's two 2x2x2 levels (k = 1, 3) assume 5 scales per octave
-    if (out->max_scale != 5) return SURFHIP_ERR_UNSUPPORTED;
+    // scales per octave: MAX_SCALE (surfd.h:9) bounds them; below 4 the
+    // octaves > 0 compute fewer than 2 scales and the lobes degenerate
+    if (out->max_scale < 4 || out->max_scale > kMaxScale) return SURFHIP_ERR_UNSUPPORTED;
     if (out->nfeatures > 128) return SURFHIP_ERR_UNSUPPORTED;
     return SURFHIP_OK;
 }
@@ -335,6 +336,8 @@ static int derive(surfhip_detector* d)
             q.psp = d->oct[o - 1].sp;
             q.posize = d->oct[o - 1].osize;
             q.pooff = d->oct[o - 1].ooff;
+            q.half[0] = p.max_scale - 3;
+            q.half[1] = p.max_scale - 1;
         } else {
             border1 = ((3 * (mask_size + 6 * octave)) / 2) / (p.sampling * octave) + 1;
             s = 0;

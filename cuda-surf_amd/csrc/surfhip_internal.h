@@ -48,11 +48,13 @@ struct OctaveParams {
     int mask[kMaxScale], b1[kMaxScale], x2[kMaxScale], x3[kMaxScale], x4[kMaxScale];
     float norm[kMaxScale];
     int borders[kMaxScale];         // host borders[] (d_borders), index s
-    int mb[2];                      // NMS start offsets (maximum_borders)
+    int mb[(kMaxScale - 2) / 2];    // NMS start offsets (maximum_borders, one per level)
     int nms_gx, nms_gy;             // NMS launch extent in threads
-    // previous octave (source of the halfImage planes 0 and 1)
+    // previous octave (source of the halfImage planes 0 and 1: its planes
+    // max_scale - 3 and max_scale - 1, surf.cpp:252-258)
     int psp, posize;
     long long pooff;
+    int half[2];
 };
 
 // Frame-level parameters (SurfParam + integral geometry).

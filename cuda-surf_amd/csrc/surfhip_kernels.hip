@@ -1046,7 +1046,7 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
                 hb += plan.hess_nbx[o] * ((q.sh + 3) / 4);
             plan.nms_nbx[o] = (q.nms_gx + 63) / 64;
             plan.nms_nby[o] = (q.nms_gy + kScanRows - 1) / kScanRows;
-            nb += 2 * plan.nms_nbx[o] * plan.nms_nby[o];
+            nb += ((P.max_scale - 1) / 2) * plan.nms_nbx[o] * plan.nms_nby[o];   // levels k = 1, 3, .. < max_scale - 1
         } else {
             plan.hess_nbx[o] = plan.nms_nbx[o] = plan.nms_nby[o] = 1;
         }
@@ -1517,13 +1517,14 @@ struct OctView {
     const float* F;                 // the frame's response block
     int cur, prev;                  // float offsets of this octave's / the previous octave's plane 0 (-1: none)
     int sp, osize, psp, posize;
+    int h0, h1;                     // halfImage sources: planes max_scale - 3 / - 1 of the previous octave
     // branch-free (selects): a branch around a load makes hipcc wait for the
     // loads issued before it at the join, which serialised the NMS scan's 32
     // block loads into 16 memory round trips
     __device__ __forceinline__ int off(int s, int r, int c) const
     {
         const bool h = prev >= 0 && s < 2;          // planes 0/1 of octave > 0: previous octave, 2x stride
-        const int base = h ? prev + (s == 0 ? 2 : 4) * posize : cur + s * osize;
+        const int base = h ? prev + (s == 0 ? h0 : h1) * posize : cur + s * osize;
         return base + r * (h ? 2 * psp : sp) + (h ? 2 * c : c);
     }
     __device__ __forceinline__ float operator()(int s, int r, int c) const { return F[off(s, r, c)]; }
@@ -1685,6 +1686,8 @@ __device__ __forceinline__ OctView make_view(const float* F, const OctaveParams&
     V.osize = q.osize;
     V.psp = q.psp;
     V.posize = q.posize;
+    V.h0 = q.half[0];
+    V.h1 = q.half[1];
     return V;
 }
 
@@ -1837,7 +1840,8 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
             if (ok) {
                 const int slot = nsurv + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mo >> 32),
                                                                        __builtin_amdgcn_mbcnt_lo((unsigned)mo, 0u));
-                rkey[slot] = ((uint32_t)o << 29) | ((uint32_t)z << 28) | ((uint32_t)y << 14) | (uint32_t)xx;
+                // (octave 3 bits, level 2, block row 13, block column 14): the canonical order
+                rkey[slot] = ((uint32_t)o << 29) | ((uint32_t)z << 27) | ((uint32_t)y << 14) | (uint32_t)xx;
                 rsrc_[slot] = ((uint32_t)s << 28) | ((uint32_t)r << 14) | (uint32_t)c;
                 if (CUBE && slot < kCubeCap) {
                     // the 19 values fitQuadrat's first pass reads (fit_quad),

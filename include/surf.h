@@ -47,5 +47,6 @@ namespace surf
         int3 whp{0, 0, 0};
         surfhip_detector* det = nullptr;      // scratch sized for (whp.x, whp.y)
         int det_w = 0, det_h = 0, det_pts = 0;
+        bool warned_trunc = false;            // candidate-capacity truncation reported
     };
 }

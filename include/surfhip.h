@@ -107,7 +107,8 @@ typedef struct surfhip_detector surfhip_detector;
 
 /* Surfor::init + allocMemory (surf.cpp:60-91, 374-415).  `param` must come
  * from surfhip_make_param.  cand_cap = per-frame candidate capacity before
- * the canonical sort (0 = default 65536).  stream = hipStream_t or NULL. */
+ * the canonical sort, rounded up to a power of 2 (0 = max(max_pts, 16384)).
+ * stream = hipStream_t or NULL. */
 int surfhip_detector_create(surfhip_detector** det, const surfhip_param* param,
                             int width, int height, int max_batch, int max_pts,
                             int cand_cap, void* stream);
@@ -139,7 +140,12 @@ int surfhip_detect_batch(surfhip_detector* det, const uint8_t* d_frames, int nfr
 /* Surfor::detectAndCompute (surf.cpp:205-355) for one frame, synchronous.
  * Writes min(found, max_pts) SurfPoints to d_points, returns the count in
  * *num_pts; when desc != 0 allocates *d_desc_out = num_pts*nfeatures floats
- * (caller frees with surfhip_free, as main.cpp:275-282 does with cudaFree). */
+ * (caller frees with surfhip_free, as main.cpp:275-282 does with cudaFree).
+ * A frame with more NMS survivors than the candidate capacity returns
+ * SURFHIP_OK with the first cand_cap survivors in scan order (as the
+ * reference returns some max_pts points without a signal, surfd.cu:822-831):
+ * callers that must know query surfhip_detector_status (the C++ Surfor
+ * prints a warning). */
 int surfhip_detect(surfhip_detector* det, const uint8_t* d_image, int pitch,
                    surfhip_point* d_points, int max_pts, int* num_pts,
                    float** d_desc_out, int desc);
@@ -203,7 +209,10 @@ size_t surfhip_slab_bytes(int nframes, int total, int nfeatures);
 int surfhip_batch_total(surfhip_detector* det, int nframes, int* total);
 int surfhip_pack_slab(surfhip_detector* det, const surfhip_point* d_points, const float* d_desc,
                       const int* d_counts, int nframes, void* d_slab);
-/* The same into a buffer of cap_bytes, with no host synchronisation: the
+/* Both pack functions read the detector's per-batch offsets and status
+ * word: enqueue them on the detector's stream BEFORE the next detect_batch
+ * (which resets both), as bench.py and the ingest ring do.
+ * The same into a buffer of cap_bytes, with no host synchronisation: the
  * multi-GPU path sizes every rank's slab once (a per-frame keypoint budget,
  * SURVEY.md 8e) and all-gathers that many bytes per batch.  A batch that
  * does not fit writes its header and counts with flags bit 1 set and no

@@ -43,7 +43,7 @@ class Octave(C.Structure):
     _fields_ = [("octave", C.c_int), ("init_scale", C.c_int), ("nscale", C.c_int), ("delta", C.c_int),
                 ("mask", C.c_int * 8), ("border1", C.c_int * 8), ("x2", C.c_int * 8),
                 ("x3", C.c_int * 8), ("x4", C.c_int * 8), ("norm", C.c_float * 8),
-                ("borders", C.c_int * 8), ("mborders", C.c_int * 2), ("nms_gx", C.c_int),
+                ("borders", C.c_int * 8), ("mborders", C.c_int * 3), ("nms_gx", C.c_int),
                 ("nms_gy", C.c_int)]
 
 

@@ -64,7 +64,9 @@ int or_init_param(or_param* p, int noctaves, float thresh, bool doubled,
     p->mag_factor = 12 / desc_wsz;
     p->orient_size = 4 + (extend ? 4 : 0);
     p->nfeatures = desc_wsz * desc_wsz * p->orient_size;
-    if (p->max_scale != 5) return -1;             /* NMS levels assume 5 scales */
+    /* scales per octave: MAX_SCALE bounds them (surfd.h:9); below 4 the
+     * octaves > 0 compute fewer than 2 scales and the lobes degenerate */
+    if (p->max_scale < 4 || p->max_scale > OR_MAX_SCALE) return -1;
     return 0;
 }
 
@@ -288,12 +290,13 @@ void or_hessian(const or_param* p, const or_geom* g, const or_octave* oct,
         const int sw = g->swhp[o].x, sh = g->swhp[o].y, sp = g->swhp[o].z;
         float* base = resp + g->ooff[o];
         if (o > 0) {
-            /* dof0 <- sof0 (plane 2 of o-1), dof1 <- sof1 (plane 4 of o-1) */
+            /* dof0 <- sof0 (plane max_scale - 3 of o-1), dof1 <- sof1 (plane
+             * max_scale - 1; surf.cpp:252-258: offset - 3 / - 1 planes) */
             const float* prev = resp + g->ooff[o - 1];
             const int pp = g->swhp[o - 1].z;
             const size_t pos = (size_t)g->osize[o - 1];
             for (int t = 0; t < 2; t++) {
-                const float* src = prev + (t == 0 ? 2 : 4) * pos;
+                const float* src = prev + (size_t)(t == 0 ? p->max_scale - 3 : p->max_scale - 1) * pos;
                 float* dst = base + (size_t)t * g->osize[o];
                 memset(dst, 0, sizeof(float) * g->osize[o]);
                 for (int iy = 0; iy < sh; iy++)
@@ -534,7 +537,8 @@ int or_find_points(const or_param* p, const or_geom* g, const or_octave* oct,
     for (int o = 0; o < p->noctaves; o++) {
         const or_octave* q = &oct[o];
         const float* src = resp + g->ooff[o];
-        for (int z = 0; z < 2; z++)
+        /* grid z = the NMS levels k = 1, 3, .. < max_scale - 1 (surfd.cu:3064-3071) */
+        for (int z = 0; z < (p->max_scale - 1) / 2; z++)
             for (int y = 0; y < q->nms_gy; y++)
                 for (int x = 0; x < q->nms_gx; x++) {
                     or_point pt;

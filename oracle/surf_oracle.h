@@ -100,7 +100,7 @@ typedef struct {
     int x2[OR_MAX_SCALE], x3[OR_MAX_SCALE], x4[OR_MAX_SCALE];
     float norm[OR_MAX_SCALE];
     int borders[OR_MAX_SCALE];        /* host borders[] (d_borders), index s */
-    int mborders[2];                  /* NMS start offsets (maximum_borders) */
+    int mborders[3];                  /* NMS start offsets (maximum_borders[(MAX_SCALE - 2) / 2]) */
     int nms_gx, nms_gy;               /* NMS launch extent in threads        */
 } or_octave;
 

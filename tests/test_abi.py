@@ -83,9 +83,22 @@ def test_make_param_matches_oracle(surf, orc):
 
 def test_make_param_rejects_out_of_scope(surf):
     with pytest.raises(surf.SurfError):
-        surf.make_param(4, 4.0, init_mask_size=12)     # max_scale != 5
+        surf.make_param(4, 4.0, init_mask_size=21)     # max_scale 9 > MAX_SCALE (surfd.h:9)
+    with pytest.raises(surf.SurfError):
+        surf.make_param(4, 4.0, init_mask_size=5)      # max_scale 3: degenerate lobes
     with pytest.raises(surf.SurfError):
         surf.make_param(0, 4.0)
+
+
+@pytest.mark.parametrize("init_mask", [6, 9, 12, 15, 18, 20])
+def test_make_param_init_mask_sizes_match_oracle(surf, orc, init_mask):
+    """Surfor::init with the reference's other initial lobes (main.cpp:195:
+    lobe 5 = init_mask_size 15 for doubled images): max_scale = lobe + 2,
+    4 .. MAX_SCALE."""
+    for dbl in (False, True):
+        a = surf.make_param(4, 4.0, dbl, init_mask, 2, True, False, 4)
+        b = orc.make_param(4, 4.0, dbl, init_mask, 2, True, False, 4)
+        assert bytes(a) == bytes(b) and a.max_scale == init_mask // 3 + 2
 
 
 def test_errors_without_gpu_are_reported(surf):

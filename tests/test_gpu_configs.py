@@ -165,3 +165,82 @@ def test_gather_plan_cases(surf, orc, monkeypatch, case):
         o_pts, o_desc, _ = orc.detect(op, frames[f], w, h)
         assert len(o_pts) > 50
         compare_frame(res["pts"][f], res["desc"][f], o_pts, o_desc, upright)
+
+
+@pytest.mark.parametrize("init_mask,doubled", [(15, True), (15, False), (12, False), (18, False), (6, False)])
+def test_init_mask_sizes(surf, orc, init_mask, doubled):
+    """Surfor::init's other initial lobes (surf.cpp:63-65: max_scale =
+    init_mask_size / 3 + 2): lobe 5 (init_mask_size 15, 7 scales, 3 NMS levels)
+    is main.cpp:195's setting for doubled images.  Planes bit-exact (the
+    gather Hessian: the streaming kernels are compiled for lobe 3), keypoints
+    bit-exact, descriptors within 1e-4 (halfImage from planes max_scale - 3 /
+    max_scale - 1, NMS over levels k = 1, 3, .. < max_scale - 1)."""
+    w, h = 640, 480
+    frames = surf.synth_frames(2, w, h, first=90)
+    param = surf.make_param(4, 2.0, doubled=doubled, init_mask_size=init_mask, upright=True)
+    assert param.max_scale == init_mask // 3 + 2
+    res = gpu_run(surf, param, frames, w, h, want_ws=True)
+    op = orc.make_param(4, 2.0, doubled, init_mask, 2, True, False, 4)
+    from test_gpu_parity import _plane_views
+    for f in range(2):
+        img = frames[f]
+        _, ref, g, octs = orc.hessian(op, img, w, h)
+        for (o, s, rp), (_, _, gp) in zip(_plane_views(ref, g, octs, op), _plane_views(res["resp"][f], g, octs, op)):
+            same = rp.view(np.uint32) == gp.view(np.uint32)
+            assert same.all(), f"octave {o} scale {s}: {(~same).sum()} cells differ"
+        o_pts, o_desc, nc = orc.detect(op, img, w, h)
+        assert len(o_pts) > 20
+        assert res["cand"][f] == nc
+        compare_frame(res["pts"][f], res["desc"][f], o_pts, o_desc, True)
+
+
+def test_config5_per_rank_batch(surf, orc, monkeypatch):
+    """Config #5 at the size one of its 8 ranks runs (bench.py): 64 frames of
+    3840x2160, 5 octaves, rotated, 128-D, max_pts 262,144 -- frames 0, 7, 8,
+    31, 63 against the oracle and all 64 against a single-frame detector (the
+    gather plan: an independent Hessian path)."""
+    w, h, n, max_pts, nf = 3840, 2160, 64, 262144, 128
+    frames = surf.synth_frames(n, w, h, first=0)
+    pitch = frames.shape[2]
+    param = surf.make_param(5, 4.0, upright=False, extend=True)
+    det = surf.Detector(param, w, h, max_batch=n, max_pts=max_pts)
+    fb = surf.DeviceBuffer(frames.nbytes)
+    fb.upload(frames)
+    pb = surf.DeviceBuffer(48 * n * max_pts)
+    db = surf.DeviceBuffer(4 * n * max_pts * nf)
+    cb = surf.DeviceBuffer(4 * n)
+    det.detect_batch(fb.ptr, n, pitch, h * pitch, pb.ptr, db.ptr, cb.ptr)
+    surf.synchronize()
+    counts = cb.download(np.int32, n)
+    assert not det.truncated() and (counts < max_pts).all() and counts.min() > 5000
+    cand = det.candidates(n)
+    det.close()
+
+    def frame_out(f):
+        c = int(counts[f])
+        pts = pb.download(surf.POINT_DTYPE, c, offset=48 * f * max_pts)
+        d = db.download(np.float32, c * nf, offset=4 * f * max_pts * nf).reshape(c, nf)
+        return pts, d
+
+    op = orc.make_param(5, 4.0, upright=False, extend=True)
+    for f in (0, 7, 8, 31, 63):
+        o_pts, o_desc, nc = orc.detect(op, frames[f], w, h, max_pts=max_pts)
+        assert cand[f] == nc
+        pts, d = frame_out(f)
+        compare_frame(pts, d, o_pts, o_desc, False)
+    monkeypatch.delenv("SURFHIP_HESS_GATHER", raising=False)
+    one = surf.Detector(param, w, h, max_batch=1, max_pts=max_pts)
+    f1 = surf.DeviceBuffer(frames[0].nbytes)
+    p1 = surf.DeviceBuffer(48 * max_pts)
+    d1 = surf.DeviceBuffer(4 * max_pts * nf)
+    c1 = surf.DeviceBuffer(4)
+    for f in range(n):
+        f1.upload(frames[f])
+        one.detect_batch(f1.ptr, 1, pitch, 0, p1.ptr, d1.ptr, c1.ptr)
+        surf.synchronize()
+        c = int(c1.download(np.int32, 1)[0])
+        assert c == counts[f], f
+        pts, d = frame_out(f)
+        assert_points_equal(p1.download(surf.POINT_DTYPE, c), pts)
+        assert d1.download(np.float32, c * nf).tobytes() == d.tobytes(), f
+    one.close()
