@@ -405,7 +405,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
                             int max_batch, int max_pts, int cand_cap, void* stream)
 {
     if (!out || !param || width < 16 || height < 16 || max_batch < 1 || max_pts < 1) return SURFHIP_ERR_INVALID;
-    if (width + 1 > 4096) return SURFHIP_ERR_UNSUPPORTED;     // integral kernel: <= 16 columns per thread
+    if (width + 1 > 8192) return SURFHIP_ERR_UNSUPPORTED;     // integral kernels: <= 32 columns per thread
     surfhip_param chk;
     int rc = surfhip_make_param(&chk, param->noctaves, param->thresh, param->doubled, param->init_lobe * 3,
                                 param->doubled ? param->sampling / 2 : param->sampling, param->upright,
@@ -419,7 +419,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     // (2W-2) x (2H-2) upsampled frames D, giving the (2W-1) x (2H-1) grid
     d->W = chk.doubled ? 2 * width - 2 : width;
     d->H = chk.doubled ? 2 * height - 2 : height;
-    if (d->W + 1 > 4096) {
+    if (d->W + 1 > 8192) {
         delete d;
         return SURFHIP_ERR_UNSUPPORTED;
     }
@@ -438,7 +438,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
         return rc;
     }
     d->nbands = (d->H + kBandRows - 1) / kBandRows;
-    d->CW = (d->W + 1 <= 2048) ? 2048 : 4096;
+    d->CW = (d->W + 1 <= 2048) ? 2048 : (d->W + 1 <= 4096 ? 4096 : 8192);
     const size_t B = (size_t)max_batch;
 #define ALLOC(ptr, bytes)                                    \
     do {                                                     \

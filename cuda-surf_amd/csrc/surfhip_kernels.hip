@@ -183,6 +183,12 @@ __device__ __forceinline__ void load_px(const uint8_t* row, int x0, int W, uint3
         const uint32_t w[2] = {v.x, v.y};
 #pragma unroll
         for (int k = 0; k < 8; k++) px[k] = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+    } else if constexpr (CPT == 32) {
+        const uint4 a = *reinterpret_cast<const uint4*>(row + x0);
+        const uint4 b = *reinterpret_cast<const uint4*>(row + x0 + 16);
+        const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int k = 0; k < 32; k++) px[k] = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
     } else {
         const uint4 v = *reinterpret_cast<const uint4*>(row + x0);
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -460,6 +466,14 @@ hipError_t launch_integral(const uint8_t* frames, int pitch, long long fstride, 
         k_ii_bandscan<<<dim3((W + 255) / 256, nframes), 256, 0, s>>>(colsum, nbands, CW, W);
         k_ii_fill_w<16><<<(nbands * nframes + 3) / 4, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum,
                                                                      CW, ii, P.ip, P.ii_stride, nframes, br);
+    } else if (W + 1 <= 8192) {
+        // wide frames (up to 8,191 columns): 32 columns per thread, the
+        // workgroup-scan fill (one 256-thread block per band, two barriers a row)
+        const int CW = 8192;
+        k_ii_bandsum<32><<<grid, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW, br);
+        k_ii_bandscan<<<dim3((W + 255) / 256, nframes), 256, 0, s>>>(colsum, nbands, CW, W);
+        k_ii_fill<32><<<grid, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW, ii, P.ip, P.ii_stride,
+                                           br);
     } else {
         return hipErrorInvalidValue;
     }

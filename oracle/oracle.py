@@ -217,4 +217,6 @@ def ref_host():
     L.ref_fit.restype = C.c_float
     L.ref_fit.argtypes = [_vp, _vp, _i, _i, _i, _i, _i]
     L.ref_hessian_params.argtypes = [_i, _i, _i, _i, C.POINTER(_i), _i, _vp, _i, _i, _vp, _vp]
+    L.ref_init_lut.argtypes = [_vp, _vp]
+    L.ref_octave_plan.argtypes = [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]
     return L

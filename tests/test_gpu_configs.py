@@ -244,3 +244,27 @@ def test_config5_per_rank_batch(surf, orc, monkeypatch):
         assert_points_equal(p1.download(surf.POINT_DTYPE, c), pts)
         assert d1.download(np.float32, c * nf).tobytes() == d.tobytes(), f
     one.close()
+
+
+@pytest.mark.parametrize("w,h,batch", [(5000, 360, 1), (8191, 200, 2)])
+def test_wide_frames(surf, orc, w, h, batch):
+    """Frames wider than 4,095 columns (the integral's 32-columns-per-thread
+    path): integral and planes bit-exact, keypoints bit-exact, descriptors
+    within 1e-4 (streaming Hessian kernels: conftest sets
+    SURFHIP_HESS_GATHER=0)."""
+    frames = surf.synth_frames(batch, w, h, first=300)
+    param = surf.make_param(4, 4.0, upright=True)
+    res = gpu_run(surf, param, frames, w, h, want_ws=True)
+    op = orc.make_param(4, 4.0, upright=True)
+    from test_gpu_parity import _plane_views
+    for f in range(batch):
+        ii_ref, ref, g, octs = orc.hessian(op, frames[f], w, h)
+        ip = g.iwhp.z
+        got_ii = res["ii"][f][: (h + 1) * ip].reshape(h + 1, ip)[:, : w + 1]
+        assert np.array_equal(got_ii, ii_ref.reshape(h + 1, ip)[:, : w + 1])
+        for (o, s, rp), (_, _, gp) in zip(_plane_views(ref, g, octs, op), _plane_views(res["resp"][f], g, octs, op)):
+            same = rp.view(np.uint32) == gp.view(np.uint32)
+            assert same.all(), f"octave {o} scale {s}: {(~same).sum()} cells differ"
+        o_pts, o_desc, nc = orc.detect(op, frames[f], w, h)
+        assert len(o_pts) > 100
+        compare_frame(res["pts"][f], res["desc"][f], o_pts, o_desc, True)

@@ -621,6 +621,55 @@ def test_oracle_octave_params_pinned_to_reference_host_code(orc, noct, sampling,
         octave += octave
 
 
+def test_oracle_luts_pinned_to_reference_init_lut(orc):
+    """or_init_tables' lookup1 / lookup2 against initLut's own loops
+    (surf.cpp:358-371, host expf) bit for bit; the GPU detector uploads the
+    same host values (surfhip_api.hip)."""
+    L = _ref_or_skip(orc)
+    t1 = np.zeros(83, np.float32)
+    t2 = np.zeros(40, np.float32)
+    L.ref_init_lut(t1.ctypes.data, t2.ctypes.data)
+    l1 = np.zeros(83, np.float32)
+    l2 = np.zeros(40, np.float32)
+    b = np.zeros(72, np.float32)
+    orc.lib.or_init_tables(l1.ctypes.data, l2.ctypes.data, b.ctypes.data)
+    assert l1.tobytes() == t1.tobytes() and l2.tobytes() == t2.tobytes()
+
+
+@pytest.mark.parametrize("init_mask", [6, 9, 12, 15, 18, 20])
+@pytest.mark.parametrize("sampling,doubled,noct", [(2, False, 4), (2, True, 5), (1, False, 6), (3, False, 4)])
+def test_oracle_octave_plan_pinned_to_reference_loop(orc, init_mask, sampling, doubled, noct):
+    """Every octave's borders (the NMS's d_borders) and Hessian parameters
+    from the reference's own statements (surf.cpp:240 / 261 / 269 in
+    surf.cpp:241-293's loop around surfd.cu:2833-2866) against
+    or_octave_params, for every initial lobe the reference accepts."""
+    L = _ref_or_skip(orc)
+    p = orc.make_param(noct, 4.0, doubled, init_mask, sampling, True, False, 4)
+    g, octs = orc.geometry(p, 1920, 1080)
+    ms = 8
+    swx = np.array([g.swhp[o].x for o in range(noct)], np.int32)
+    swy = np.array([g.swhp[o].y for o in range(noct)], np.int32)
+    borders = np.zeros((noct, 8), np.int32)
+    params = np.zeros((noct, 7 * ms), np.int32)
+    norms = np.zeros((noct, ms), np.float32)
+    L.ref_octave_plan(p.init_lobe, p.sampling, noct, p.max_scale, swx.ctypes.data, swy.ctypes.data,
+                      borders.ctypes.data, params.ctypes.data, norms.ctypes.data)
+    for o in range(noct):
+        q = octs[o]
+        nsc = q.nscale
+        assert nsc == p.max_scale - (0 if o == 0 else 2)
+        assert list(q.mask)[:nsc] == params[o, :nsc].tolist(), o
+        assert list(q.border1)[:nsc] == params[o, ms:ms + nsc].tolist(), o
+        assert list(q.x2)[:nsc] == params[o, 4 * ms:4 * ms + nsc].tolist()
+        assert list(q.x3)[:nsc] == params[o, 5 * ms:5 * ms + nsc].tolist()
+        assert list(q.x4)[:nsc] == params[o, 6 * ms:6 * ms + nsc].tolist()
+        assert np.array(list(q.norm)[:nsc], np.float32).tobytes() == norms[o, :nsc].tobytes()
+        assert list(q.borders)[:p.max_scale] == borders[o, :p.max_scale].tolist(), o
+        # the NMS start offsets (surfd.cu:3062-3068) from the same borders
+        lev = [k for k in range(1, p.max_scale - 1, 2)]
+        assert list(q.mborders)[:len(lev)] == [int(borders[o, k + 1]) + 1 for k in lev]
+
+
 def test_oracle_sanitizer_build():
     """ASan + UBSan build of the oracle over every mode."""
     import subprocess
