@@ -52,7 +52,6 @@ struct surfhip_detector {
     OctaveParams oct[kMaxOct]{};
     OctaveParams* d_oct = nullptr;      // device copy read by the fused launches
     LaunchPlan plan{};
-    FarPlan far{};
     int W = 0, H = 0, max_batch = 0, max_pts = 0, cap = 0;   // W x H: the frames the integral is taken of
     int srcW = 0, srcH = 0;             // the caller's frames (= W x H unless doubled)
     uint8_t* dbl = nullptr;             // doubled: the (2 srcW - 2) x (2 srcH - 2) frames D
@@ -445,7 +444,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
         e = hipMalloc((void**)&(ptr), (bytes));              \
         if (e != hipSuccess) goto fail;                      \
     } while (0)
-    make_plan(d->P, d->oct, d->plan, d->far, max_batch);
+    make_plan(d->P, d->oct, d->plan, max_batch);
     ALLOC(d->d_oct, sizeof(OctaveParams) * kMaxOct);
     ALLOC(d->ii, B * d->P.ii_stride * sizeof(int32_t));
     ALLOC(d->resp, B * d->tot_osize * sizeof(float));
@@ -562,7 +561,7 @@ int surfhip_run_hessian(surfhip_detector* d, int nframes)
 {
     if (!d || nframes < 1 || nframes > d->max_batch) return SURFHIP_ERR_INVALID;
     HIPCHK(launch_hessian(d->last_frames, d->last_pitch, d->last_fstride, d->ii, d->resp, nframes, d->P, d->d_oct,
-                          d->oct, d->plan, d->far, d->stream));
+                          d->oct, d->plan, d->stream));
     return SURFHIP_OK;
 }
 
@@ -584,7 +583,7 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
         HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, s));
         HIPCHK(hipEventRecord(d->ev[1], s));
         HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
-                              d->plan, d->far, s));
+                              d->plan, s));
         HIPCHK(hipEventRecord(d->ev[2], s));
     } else {
         // the u8 Hessian kernels (octaves 0, 1) need no integral image: they run
@@ -595,10 +594,10 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
         HIPCHK(hipStreamWaitEvent(d->side, d->fork, 0));
         HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, d->side));
         HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
-                              d->plan, d->far, d->side, 2));
+                              d->plan, d->side, 2));
         HIPCHK(hipEventRecord(d->join, d->side));
         HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
-                              d->plan, d->far, s, 1));
+                              d->plan, s, 1));
         HIPCHK(hipStreamWaitEvent(s, d->join, 0));
     }
     HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->scan_key, d->scan_src, d->scan_cube,
@@ -719,7 +718,7 @@ long long surfhip_hessian_bytes_per_frame(surfhip_detector* d) { return d ? d->h
 int surfhip_hessian_plan(surfhip_detector* d, char* buf, int len)
 {
     if (!d) return SURFHIP_ERR_INVALID;
-    const std::string t = hessian_plan_text(d->plan, d->far, d->P);
+    const std::string t = hessian_plan_text(d->plan, d->P);
     if (buf && len > 0) {
         const size_t n = std::min((size_t)len - 1, t.size());
         memcpy(buf, t.data(), n);

@@ -79,46 +79,18 @@ hipError_t set_tables(const Tables& t);
 
 hipError_t launch_integral(const uint8_t* frames, int pitch, long long fstride, int nframes,
                            const FrameParams& P, uint32_t* colsum, int32_t* ii, hipStream_t s);
-// Block ranges of the fused all-octave launches (computed once per detector).
+// Block ranges of the fused all-octave launches and the Hessian kernel of
+// each octave (computed once per detector; make_plan).
 struct LaunchPlan {
-    int hess_start[kMaxOct + 1];    // Hessian blocks of octave o: [start[o], start[o+1])
+    int hess_start[kMaxOct + 1];    // k_hessian blocks of octave o: [start[o], start[o+1])
     int hess_nbx[kMaxOct];          // blocks per row of samples
-    int nms_start[kMaxOct + 1];     // NMS blocks of octave o (both levels)
+    int nms_start[kMaxOct + 1];     // NMS blocks of octave o (every level)
     int nms_nbx[kMaxOct], nms_nby[kMaxOct];
-    int o0_lds;                     // octave 0 on the LDS-tiled kernel (k_hess_o0)
-    int o0_nbx, o0_blocks;
-    int o0_v, o0_vstrips;           // octave 0 on the u8 vertical-streaming kernel (k_hess_v0)
-    int o0_split;                   // octave-0 kernel variant (make_plan; 44 = k_hess_q0 default, 0 = k_hess_v0)
-    int o1_lds;                     // octave 1 on the LDS ring (k_hess_o1)
-    int o1_v, o1_vstrips;           // octave 1 on the u8 vertical-streaming kernel (k_hess_v1)
-    int o1_q;                       // ... its packed-fp32 variant (k_hess_q1)
-    int o01;                        // q0 and q1 in one launch (k_hess_q01)
-    int vfar_n;                     // octaves 2 .. 1 + vfar_n on k_hess_vfar (u8 vertical streaming)
-    int o1_nbx;
+    int q0, q0_strips;              // octave 0 on k_hess_q0 (u8 vertical streaming), 64-sample strips
+    int q1, q1_strips;              // octave 1 on k_hess_q1 (when k_hess_w is off)
+    int q01;                        // q0 and q1 in one launch (k_hess_q01)
     int hw_n;                       // octaves 1 .. hw_n on k_hess_w (u8, shared strip integral); 0: off
     int hw_nstrips, hw_nblk;        // its strips per frame and blocks of 4 integral rows
-};
-// Octaves >= 2 on the streaming-accumulation kernel (k_hess_far): per far
-// octave, the corner terms of every (scale, dxx/dyy/dxy) sum grouped by
-// corner row (dr) and bucketed by dr mod delta; see surfhip_kernels.hip.
-namespace farc {
-constexpr int MAXO = 3;             // far octaves on the kernel (2, 3, 4)
-constexpr int STRIP_W = 512;        // image columns per workgroup strip (one sample per lane at delta 8)
-constexpr int STRIP_N = 256;        // ... when the wide strip's accumulators do not fit LDS (5+ octaves)
-#ifndef SURF_FAR_R
-#define SURF_FAR_R 16
-#endif
-constexpr int R = SURF_FAR_R;       // image rows per step (one wave each; 8 or 16)
-constexpr int THREADS = 64 * R;
-constexpr int NA = 24;              // accumulator rows (sample rows in flight: <= 21 at R = 16)
-}
-struct FarOct {
-    int o, d, nS, drmax, accoff;    // accoff: int offset of the [NA][9][nS] accumulators
-};
-struct FarPlan {
-    int nfar;                       // 0: no far kernel
-    int H, strip, nstrips, nsteps, lds_bytes, acc_total;
-    FarOct oc[farc::MAXO];
 };
 // max_batch <= kGatherBatch (or SURFHIP_HESS_GATHER=1; =0 disables) puts every
 // octave on the one-thread-per-response gather kernel: the streaming kernels
@@ -126,14 +98,15 @@ struct FarPlan {
 // frames (measured crossover, 1080p: gather 9,956 vs streaming 7,981 frames/s
 // at 8 frames, 12,474 vs 14,085 at 16).
 constexpr int kGatherBatch = 8;
-void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, FarPlan& far, int max_batch);
+void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, int max_batch);
 // the Hessian stage's kernels of a plan, as text (surfhip_hessian_plan)
-std::string hessian_plan_text(const LaunchPlan& plan, const FarPlan& far, const FrameParams& P);
+std::string hessian_plan_text(const LaunchPlan& plan, const FrameParams& P);
 
-// frames may be null (no u8 source known): every octave then reads the integral image
+// parts: 1 = the u8-frame kernels (frames must be given), 2 = the
+// integral-image kernel (k_hessian), 3 = both
 hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, const int32_t* ii, float* resp,
                           int nframes, const FrameParams& P, const OctaveParams* d_oct, const OctaveParams* h_oct,
-                          const LaunchPlan& plan, const FarPlan& far, hipStream_t s, int parts = 3);
+                          const LaunchPlan& plan, hipStream_t s, int parts = 3);
 // NMS scan items: one wave's 64 block columns x kScanRows / 4 block rows;
 // each item owns kItemCap survivor slots (no atomics in the scan).
 hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,

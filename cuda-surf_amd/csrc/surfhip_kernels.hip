@@ -518,351 +518,14 @@ __device__ __forceinline__ float hessian_at(const uint32_t* __restrict__ I, int 
     return rr * (a - b);
 }
 
-// ----------------------------------------------------------------------
-// Octave 0 (sampling 2 => 2 px between samples, lobes 3..11): LDS ring.
-// 85 % of all responses live here and every integral value is re-read ~40
-// times.  A workgroup owns a vertical strip of 128 sample columns of one
-// frame and walks it top to bottom, streaming the integral rows through an
-// LDS ring of 64 rows: each image row of the strip is read from HBM once
-// (column halo 1.125x), and the loads of the next 16 rows are in flight while
-// the 8 waves compute the current 8 sample rows.
-// Row layout: parity planes (even / odd image columns) of *pairs*
-//   T[slot][p][k] = (I[row][xs + 2k + p], I[row][xs + 2k + p + 128])
-// so lane l, which owns samples ix and ix + 64 (x0 and x0 + 128 px), gets
-// both samples' corner with ONE conflict-free ds_read_b64 whose column offset
-// is a compile-time immediate (the lobe geometry is fixed for init_lobe 3);
-// the ring slot of a corner row is wave-uniform (scalar ALU).
-// 64 slots x 2 planes x 80 pairs x 8 B = 80 KiB -> two workgroups per CU.
-// ----------------------------------------------------------------------
-namespace o0 {
-constexpr int TXS = 128;                 // sample columns per strip (64 lanes x 2)
-constexpr int NK = 80;                   // pairs per parity-plane row
-constexpr int ROWQ = 2 * NK;             // uint64 per ring slot
-constexpr int NRING = 64;                // ring slots (image rows)
-constexpr int STEP = 16;                 // image rows per step = 8 sample rows
-constexpr int ITEMS = STEP * 40;         // fill items per step: (row, 4-column group)
-constexpr int THREADS = 512;
-}
-
-// LDS-qualified volatile view: volatile stops hipcc from pairing neighbouring
-// reads into ds_read2_b64 (half the bandwidth of ds_read_b64 on gfx950);
-// the explicit address space keeps them ds_ (a plain volatile* goes flat_).
-typedef const volatile uint64_t __attribute__((address_space(3))) lds_u64;
-
-template <int M, int X2, int X3, int X4>
-__device__ __forceinline__ void hess_pair(const lds_u64* Tl, int sb, float norm, float& ha, float& hb)
-{
-    // corner (dr, dc) relative to (y0, x0); slot sb holds image row y0 - 16,
-    // Tl points at pair `lane` of slot 0
-#define C(dr, dc) Tl[((sb + 16 + (dr)) & (o0::NRING - 1)) * o0::ROWQ + ((dc) & 1) * o0::NK + ((16 + (dc)) >> 1)]
-    const uint64_t a1 = C(X3 + 1, M + X2 + 1), a2 = C(-X3, -M - X2), a3 = C(-X3, M + X2 + 1), a4 = C(X3 + 1, -M - X2);
-    const uint64_t b1 = C(X3 + 1, X2 + 1), b2 = C(-X3, -X2), b3 = C(-X3, X2 + 1), b4 = C(X3 + 1, -X2);
-    const uint64_t c1 = C(M + X2 + 1, X3 + 1), c2 = C(-M - X2, -X3), c3 = C(-M - X2, X3 + 1), c4 = C(M + X2 + 1, -X3);
-    const uint64_t d1 = C(X2 + 1, X3 + 1), d2 = C(-X2, -X3), d3 = C(-X2, X3 + 1), d4 = C(X2 + 1, -X3);
-    const uint64_t s1a = C(1, X4 + 1), s1b = C(-X4, 0), s1c = C(-X4, X4 + 1), s1d = C(1, 0);
-    const uint64_t s2a = C(X4 + 1, 1), s2b = C(0, -X4), s2c = C(0, 1), s2d = C(X4 + 1, -X4);
-    const uint64_t s3a = C(X4 + 1, X4 + 1), s3b = C(0, 0), s3c = C(0, X4 + 1), s3d = C(X4 + 1, 0);
-    const uint64_t s4a = C(1, 1), s4b = C(-X4, -X4), s4c = C(-X4, 1), s4d = C(1, -X4);
-#undef C
-    const float rr = INV255 * INV255;
-#define LO(v) ((uint32_t)(v))
-#define HI(v) ((uint32_t)((v) >> 32))
-#define RESP(F, out)                                                                                  \
-    {                                                                                                 \
-        const uint32_t A = F(a1) + F(a2) - F(a3) - F(a4), B = F(b1) + F(b2) - F(b3) - F(b4);          \
-        const uint32_t Cc = F(c1) + F(c2) - F(c3) - F(c4), D = F(d1) + F(d2) - F(d3) - F(d4);         \
-        const uint32_t S1 = F(s1a) + F(s1b) - F(s1c) - F(s1d), S2 = F(s2a) + F(s2b) - F(s2c) - F(s2d);\
-        const uint32_t S3 = F(s3a) + F(s3b) - F(s3c) - F(s3d), S4 = F(s4a) + F(s4b) - F(s4c) - F(s4d);\
-        const float dxx = (float)(int32_t)(A - 3u * B);                                               \
-        const float dyy = (float)(int32_t)(Cc - 3u * D);                                              \
-        const float dxy = 0.6f * (float)(int32_t)(S1 + S2 - S3 - S4);                                 \
-        const float p = dxx * dyy;                                                                    \
-        const float q2 = dxy * dxy;                                                                   \
-        out = (rr * (p - q2)) * norm;                                                                 \
-    }
-    RESP(LO, ha)
-    RESP(HI, hb)
-#undef RESP
-#undef LO
-#undef HI
-}
-
-// offa / offb: byte offsets of samples ixa / ixb in plane 0 of the octave
-// (kOOB past the grid: the store is dropped)
-template <int S, int M, int X2, int X3, int X4>
-__device__ __forceinline__ void hess_store(const lds_u64* Tl, int sb, const OctaveParams& q, rsrc_t R, int iy,
-                                           int ixa, int ixb, uint32_t offa, uint32_t offb)
-{
-    float ha, hb;
-    hess_pair<M, X2, X3, X4>(Tl, sb, q.norm[S], ha, hb);
-    const int b1 = q.b1[S];
-    const bool v = iy >= b1 && iy < q.sh - b1;
-    const uint32_t po = (uint32_t)(S * q.osize) * 4u;
-    buf_st_nt(R, offa + po, (v && ixa >= b1 && ixa < q.sw - b1) ? ha : 0.f);
-    buf_st_nt(R, offb + po, (v && ixb >= b1 && ixb < q.sw - b1) ? hb : 0.f);
-}
-
-// One fill item: image row gy, columns xs + 4a .. + 3 and the same + 128.
-struct RowItem { uint4 g0, g1; };
-
-// Rows outside the image read 0 (offset past the buffer; a negative row
-// wraps to a huge unsigned offset).  Columns < 0 or >= ip read the
-// neighbouring row: they feed only samples outside every scale's valid
-// window (x0 - 16 >= 2 and x0 + 17 <= W for every valid sample of lobes
-// 3..11), whose response is written as 0.
-__device__ __forceinline__ RowItem o0_load(rsrc_t I, int ip, int gy, int gx, bool ok = true)
-{
-    const uint32_t off = ok ? (uint32_t)(gy * ip + gx) * 4u : kOOB;
-    RowItem v;
-    v.g0 = buf_ld4(I, off);
-    v.g1 = buf_ld4(I, off + 512u);
-    return v;
-}
-
-// Two dwords from independent registers into one LDS pair slot.  As an asm
-// statement, so hipcc neither merges the pair writes of an item into a
-// ds_write_b128 (whose 4-register data tuple it would assemble with copies
-// placed at the loop back-edge, waiting there for the loads still in
-// flight) nor counts it: callers drain lgkmcnt before the barrier.
-__device__ __forceinline__ void lds_write2(uint32_t addr, uint32_t a, uint32_t b)
-{
-    asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" ::"v"(addr), "v"(a), "v"(b) : "memory");
-}
-
-__device__ __forceinline__ void o0_store(uint64_t* T, int gy, int a, const RowItem& v)
-{
-    const uint32_t dst = (uint32_t)reinterpret_cast<uintptr_t>(T + (gy & (o0::NRING - 1)) * o0::ROWQ + 2 * a);
-    lds_write2(dst, v.g0.x, v.g1.x);                        // even plane, pairs 2a, 2a + 1
-    lds_write2(dst + 8u, v.g0.z, v.g1.z);
-    lds_write2(dst + 8u * o0::NK, v.g0.y, v.g1.y);          // odd plane
-    lds_write2(dst + 8u * o0::NK + 8u, v.g0.w, v.g1.w);
-}
-
-__device__ __forceinline__ void lds_drain()
-{
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
-__global__ __launch_bounds__(o0::THREADS, 4) void k_hess_o0(const int32_t* __restrict__ ii, float* __restrict__ resp,
-                                                            FrameParams P, OctaveParams q, int nstrips, int nframes)
-{
-    __shared__ __attribute__((aligned(16))) uint64_t T[o0::NRING * o0::ROWQ];
-    // XCD-aware order: the workgroups of XCD x (blockIdx % 8) take frames
-    // x, x + 8, ..., all strips of a frame together, so the strips' shared
-    // halo columns are served from that XCD's L2.
-    const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
-    const int f = (k / nstrips) * 8 + xcd, bx = k % nstrips;
-    if (f >= nframes) return;
-    const int IX0 = bx * o0::TXS;
-    const int xs = 2 * IX0 - 16;
-    const rsrc_t I = make_rsrc(ii + (size_t)f * P.ii_stride, (long long)P.iH * P.ip * 4);
-    const int ip = P.ip;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // item it of a 16-row chunk starting at image row y: row y + it / 40, group it % 40
-    const int ra0 = tid / 40, ga0 = tid - ra0 * 40;                 // it = tid          (< 640)
-    const int it1 = tid + o0::THREADS;                               // it = tid + 512    (< 640 for tid < 128)
-    const bool has1 = it1 < o0::ITEMS;
-    const int ra1 = it1 / 40, ga1 = it1 - ra1 * 40;     // threads without a second item load past the buffer
-    // ---- prologue: image rows -16 .. 31
-    for (int y = -16; y < 32; y += o0::STEP) {
-        const RowItem v0 = o0_load(I, ip, y + ra0, xs + 4 * ga0);
-        const RowItem v1 = o0_load(I, ip, y + ra1, xs + 4 * ga1, has1);
-        o0_store(T, y + ra0, ga0, v0);
-        if (has1) o0_store(T, y + ra1, ga1, v1);
-    }
-    lds_drain();
-    __syncthreads();
-    const lds_u64* Tl = (const lds_u64*)T + lane;
-    const int ixa = IX0 + lane, ixb = ixa + 64;
-    const rsrc_t R = make_rsrc(resp + (size_t)f * P.resp_stride + q.ooff, (P.resp_stride - q.ooff) * 4);
-    const int nsteps = (q.sh + 7) >> 3;
-    // Two-deep prefetch: the rows step s + 2 adds (16 s + 48 ..) are loaded
-    // at the start of step s and written to the ring at the end of step s + 1,
-    // so each load has two steps of compute to land.  The rows step s + 1
-    // adds (16 s + 32 ..) go into the slots of rows 16 s - 32 .., last read
-    // in step s - 1.  Every global load and store of the loop is issued
-    // unconditionally (past the buffer where nothing is there), so hipcc's
-    // count of outstanding ops is exact and the wait before the ring write
-    // leaves the younger loads in flight.
-    RowItem pa0, pa1, pb0, pb1;
-    pa0 = o0_load(I, ip, 32 + ra0, xs + 4 * ga0);
-    pa1 = o0_load(I, ip, 32 + ra1, xs + 4 * ga1, has1);
-    auto step = [&](int s, RowItem& cur0, RowItem& cur1, RowItem& nxt0, RowItem& nxt1) {
-        const int yl = 16 * s + 48;                 // rows loaded now, for step s + 2
-        nxt0 = o0_load(I, ip, yl + ra0, xs + 4 * ga0);
-        nxt1 = o0_load(I, ip, yl + ra1, xs + 4 * ga1, has1);
-        const int iy = 8 * s + w;
-        {
-            const int sb = (2 * iy - 16) & (o0::NRING - 1);
-            const bool rowok = iy < q.sh;
-            const uint32_t offa = (rowok && ixa < q.sw) ? (uint32_t)(iy * q.sp + ixa) * 4u : kOOB;
-            const uint32_t offb = (rowok && ixb < q.sw) ? (uint32_t)(iy * q.sp + ixb) * 4u : kOOB;
-            hess_store<0, 3, 1, 2, 3>(Tl, sb, q, R, iy, ixa, ixb, offa, offb);
-            hess_store<1, 5, 2, 4, 6>(Tl, sb, q, R, iy, ixa, ixb, offa, offb);
-            hess_store<2, 7, 3, 6, 9>(Tl, sb, q, R, iy, ixa, ixb, offa, offb);
-            hess_store<3, 9, 4, 8, 12>(Tl, sb, q, R, iy, ixa, ixb, offa, offb);
-            hess_store<4, 11, 5, 10, 15>(Tl, sb, q, R, iy, ixa, ixb, offa, offb);
-        }
-        if (s + 1 < nsteps) {
-            const int yw = 16 * s + 32;             // rows step s + 1 needs
-            o0_store(T, yw + ra0, ga0, cur0);
-            if (has1) o0_store(T, yw + ra1, ga1, cur1);
-        }
-        lds_drain();
-        __syncthreads();
-    };
-    for (int s = 0; s < nsteps; s += 2) {
-        step(s, pa0, pa1, pb0, pb1);
-        if (s + 1 < nsteps) step(s + 1, pb0, pb1, pa0, pa1);
-    }
-}
-
-#include "surfhip_hess_v0.inc"
-#include "surfhip_hess_v1.inc"
-#include "surfhip_hess_vfar.inc"
 #include "surfhip_hess_q0.inc"
 #include "surfhip_hess_q1.inc"
 #include "surfhip_hess_w.inc"
 
-// ----------------------------------------------------------------------
-// Octave 1 (4 px between samples, lobes 15/19/23: corner offsets -34..35):
-// the same strip walk with an LDS ring, one workgroup per CU.  A strip is
-// 64 sample columns (lane = sample); each ring slot holds image columns
-// xs .. xs + 323 (xs = 4 * IX0 - 36) split into 4 residue planes
-//   T[slot][c & 3][c >> 2]   (c = column - xs)
-// so the 64 lanes' reads of one corner are 64 consecutive dwords.  A step is
-// 4 sample rows (16 image rows); its window is rows y - 34 .. y + 47, and the
-// ring of 98 slots leaves room for the 16 rows of the next step.  12 waves:
-// wave (r, scale) computes one sample row of one scale per step.
-// ----------------------------------------------------------------------
-namespace o1 {
-constexpr int TXS = 64;                  // sample columns per strip
-constexpr int NK = 81;                   // dwords per residue plane
-constexpr int ROWD = 4 * NK;             // dwords per ring slot
-constexpr int NRING = 98;                // ring slots (image rows)
-constexpr int LO = 34;                   // rows above a sample row in its window
-constexpr int STEP = 16;                 // image rows per step = 4 sample rows
-constexpr int ITEMS = STEP * NK;         // fill items per step: (row, 4-column group)
-constexpr int THREADS = 768;
-}
-
-template <int M, int X2, int X3, int X4>
-__device__ __forceinline__ float hess1(const uint32_t* Tl, int sb, float norm)
-{
-    // corner (dr, dc) relative to (y0, x0); slot sb holds image row y0 - 34
-#define SLOT(dr) ((sb + LOFF + (dr)) >= o1::NRING ? (sb + LOFF + (dr)) - o1::NRING : (sb + LOFF + (dr)))
-#define C(dr, dc) Tl[SLOT(dr) * o1::ROWD + ((dc) & 3) * o1::NK + ((36 + (dc)) >> 2)]
-    constexpr int LOFF = o1::LO;
-    const uint32_t a1 = C(X3 + 1, M + X2 + 1), a2 = C(-X3, -M - X2), a3 = C(-X3, M + X2 + 1), a4 = C(X3 + 1, -M - X2);
-    const uint32_t b1 = C(X3 + 1, X2 + 1), b2 = C(-X3, -X2), b3 = C(-X3, X2 + 1), b4 = C(X3 + 1, -X2);
-    const uint32_t c1 = C(M + X2 + 1, X3 + 1), c2 = C(-M - X2, -X3), c3 = C(-M - X2, X3 + 1), c4 = C(M + X2 + 1, -X3);
-    const uint32_t d1 = C(X2 + 1, X3 + 1), d2 = C(-X2, -X3), d3 = C(-X2, X3 + 1), d4 = C(X2 + 1, -X3);
-    const uint32_t s1a = C(1, X4 + 1), s1b = C(-X4, 0), s1c = C(-X4, X4 + 1), s1d = C(1, 0);
-    const uint32_t s2a = C(X4 + 1, 1), s2b = C(0, -X4), s2c = C(0, 1), s2d = C(X4 + 1, -X4);
-    const uint32_t s3a = C(X4 + 1, X4 + 1), s3b = C(0, 0), s3c = C(0, X4 + 1), s3d = C(X4 + 1, 0);
-    const uint32_t s4a = C(1, 1), s4b = C(-X4, -X4), s4c = C(-X4, 1), s4d = C(1, -X4);
-#undef C
-#undef SLOT
-    const uint32_t A = a1 + a2 - a3 - a4, B = b1 + b2 - b3 - b4;
-    const uint32_t Cc = c1 + c2 - c3 - c4, D = d1 + d2 - d3 - d4;
-    const uint32_t S1 = s1a + s1b - s1c - s1d, S2 = s2a + s2b - s2c - s2d;
-    const uint32_t S3 = s3a + s3b - s3c - s3d, S4 = s4a + s4b - s4c - s4d;
-    const float rr = INV255 * INV255;
-    const float dxx = (float)(int32_t)(A - 3u * B);
-    const float dyy = (float)(int32_t)(Cc - 3u * D);
-    const float dxy = 0.6f * (float)(int32_t)(S1 + S2 - S3 - S4);
-    const float p = dxx * dyy;
-    const float q2 = dxy * dxy;
-    return (rr * (p - q2)) * norm;
-}
-
-// Rows outside the image read 0; columns < 0 or >= ip (the neighbouring row)
-// feed only samples outside every scale's valid window (x0 - 35 >= 1 and
-// x0 + 35 <= W for every valid octave-1 sample).
-__device__ __forceinline__ uint4 o1_load(rsrc_t I, int ip, int gy, int gx, bool ok = true)
-{
-    return buf_ld4(I, ok ? (uint32_t)(gy * ip + gx) * 4u : kOOB);
-}
-
-__device__ __forceinline__ void o1_store(uint32_t* T, int gy, int a, uint4 v)
-{
-    const int slot = (gy + 2 * o1::NRING) % o1::NRING;
-    uint32_t* dst = T + slot * o1::ROWD + a;
-    dst[0] = v.x;
-    dst[o1::NK] = v.y;
-    dst[2 * o1::NK] = v.z;
-    dst[3 * o1::NK] = v.w;
-}
-
-__global__ __launch_bounds__(o1::THREADS, 1) void k_hess_o1(const int32_t* __restrict__ ii, float* __restrict__ resp,
-                                                            FrameParams P, OctaveParams q, int nstrips, int nframes)
-{
-    __shared__ __attribute__((aligned(16))) uint32_t T[o1::NRING * o1::ROWD];
-    const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
-    const int f = (k / nstrips) * 8 + xcd, bx = k % nstrips;
-    if (f >= nframes) return;
-    const int IX0 = bx * o1::TXS;
-    const int xs = 4 * IX0 - 36;
-    const rsrc_t I = make_rsrc(ii + (size_t)f * P.ii_stride, (long long)P.iH * P.ip * 4);
-    const int ip = P.ip;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ra0 = tid / o1::NK, ga0 = tid - ra0 * o1::NK;                 // item tid
-    const int it1 = tid + o1::THREADS;                                      // item tid + 768
-    const int ra1 = it1 / o1::NK, ga1 = it1 - ra1 * o1::NK;
-    const bool has1 = it1 < o1::ITEMS;                  // threads without a second item load past the buffer
-    // ---- prologue: image rows -34 .. 47 (step 0's window)
-    for (int it = tid; it < 82 * o1::NK; it += o1::THREADS) {
-        const int r = it / o1::NK, a = it - r * o1::NK;
-        o1_store(T, r - 34, a, o1_load(I, ip, r - 34, xs + 4 * a));
-    }
-    __syncthreads();
-    const uint32_t* Tl = T + lane;
-    const int ix = IX0 + lane;
-    const rsrc_t R = make_rsrc(resp + (size_t)f * P.resp_stride + q.ooff, (P.resp_stride - q.ooff) * 4);
-    const int nsteps = (q.sh + 3) >> 2;
-    const int ur = w & 3, us = w >> 2;            // this wave's (sample row, scale) unit
-    const int b1 = q.b1[us];
-    const float norm = q.norm[us];
-    const uint32_t pofs = (uint32_t)((q.init_scale + us) * q.osize) * 4u;
-    // two-deep prefetch, as in k_hess_o0: rows 16 s + 64 .. (step s + 2) load
-    // now and land in the ring at the end of step s + 1
-    uint4 pa0 = make_uint4(0u, 0u, 0u, 0u), pa1 = pa0, pb0 = pa0, pb1 = pa0;
-    pa0 = o1_load(I, ip, 48 + ra0, xs + 4 * ga0);
-    pa1 = o1_load(I, ip, 48 + ra1, xs + 4 * ga1, has1);
-    auto step = [&](int s, uint4& cur0, uint4& cur1, uint4& nxt0, uint4& nxt1) {
-        const int yl = 16 * s + 64;
-        nxt0 = o1_load(I, ip, yl + ra0, xs + 4 * ga0);
-        nxt1 = o1_load(I, ip, yl + ra1, xs + 4 * ga1, has1);
-        const int iy = 4 * s + ur;
-        {
-            const int sb = (4 * iy - 34 + 2 * o1::NRING) % o1::NRING;
-            float h;
-            if (us == 0) h = hess1<15, 7, 14, 21>(Tl, sb, norm);
-            else if (us == 1) h = hess1<19, 9, 18, 27>(Tl, sb, norm);
-            else h = hess1<23, 11, 22, 33>(Tl, sb, norm);
-            const bool v = iy >= b1 && iy < q.sh - b1 && ix >= b1 && ix < q.sw - b1;
-            buf_st_nt(R, (iy < q.sh && ix < q.sw) ? pofs + (uint32_t)(iy * q.sp + ix) * 4u : kOOB, v ? h : 0.f);
-        }
-        if (s + 1 < nsteps) {
-            const int yw = 16 * s + 48;
-            o1_store(T, yw + ra0, ga0, cur0);
-            if (has1) o1_store(T, yw + ra1, ga1, cur1);
-        }
-        __syncthreads();
-    };
-    for (int s = 0; s < nsteps; s += 2) {
-        step(s, pa0, pa1, pb0, pb1);
-        if (s + 1 < nsteps) step(s + 1, pb0, pb1, pa0, pa1);
-    }
-}
-
-// Octave 1 takes the LDS ring when its geometry is the one compiled into
-// k_hess_o1 (sampling 2, init lobe 3: lobes 15/19/23, planes 2..4).
-static bool o1_lds_ok(const FrameParams& P, const OctaveParams& q)
+// Octave 1 on k_hess_q1 (only when k_hess_w is off: 2-octave detectors or
+// SURFHIP_HESS_W=0) needs the geometry compiled into it (sampling 2, lobes
+// 15/19/23).
+static bool q1_ok(const FrameParams& P, const OctaveParams& q)
 {
     static const int masks[3] = {15, 19, 23};
     if (P.sampling != 2 || q.delta != 4 || q.nscale != 3 || q.init_scale != 2) return false;
@@ -873,9 +536,9 @@ static bool o1_lds_ok(const FrameParams& P, const OctaveParams& q)
     return true;
 }
 
-// Octave 0 takes the LDS path when its geometry is the fixed one compiled
-// into k_hess_o0 (sampling 2, lobes 3/5/7/9/11).
-static bool o0_lds_ok(const FrameParams& P, const OctaveParams& q)
+// Octave 0 on k_hess_q0 when its geometry is the one compiled into it
+// (sampling 2, lobes 3/5/7/9/11).
+static bool q0_ok(const FrameParams& P, const OctaveParams& q)
 {
     static const int masks[5] = {3, 5, 7, 9, 11};
     if (P.sampling != 2 || q.delta != 2 || q.nscale != 5 || q.init_scale != 0) return false;
@@ -883,115 +546,6 @@ static bool o0_lds_ok(const FrameParams& P, const OctaveParams& q)
         if (q.mask[i] != masks[i] || q.x2[i] != masks[i] / 2 || q.x3[i] != 2 * (masks[i] / 2) ||
             q.x4[i] != 3 * (masks[i] / 2))
             return false;
-    return true;
-}
-
-// The corner terms of the reference's getHessian (surfd.cu:353-366) for one
-// scale, as (dr, dc, weight, slot): slot 0 = dxx sum (outer box - 3 inner),
-// 1 = dyy, 2 = dxy (S1 + S2 - S3 - S4); I(dr, dc) = ii[y0 + dr][x0 + dc].
-struct HCorner { int dr, dc, w, slot; };
-static int hessian_corners(int M, int X2, int X3, int X4, HCorner* out)
-{
-    int n = 0;
-    auto box = [&](int x1, int y1, int x2, int y2, int w, int slot) {   // getSum, surfd.cu:334-343
-        out[n++] = {y1 + 1, x1 + 1, w, slot};
-        out[n++] = {y2, x2, w, slot};
-        out[n++] = {y2, x1 + 1, -w, slot};
-        out[n++] = {y1 + 1, x2, -w, slot};
-    };
-    box(M + X2, X3, -M - X2, -X3, 1, 0);
-    box(X2, X3, -X2, -X3, -3, 0);
-    box(X3, M + X2, -X3, -M - X2, 1, 1);
-    box(X3, X2, -X3, -X2, -3, 1);
-    box(X4, 0, 0, -X4, 1, 2);
-    box(0, X4, -X4, 0, 1, 2);
-    box(X4, X4, 0, 0, -1, 2);
-    box(0, 0, -X4, -X4, -1, 2);
-    return n;
-}
-
-// Far-octave plan: octaves 2.. of the default geometry (init lobe 3,
-// sampling 2: lobes 31/39/47, 63/79/95, 127/159/191, the variants compiled
-// into surfhip_far.inc) whose accumulators fit k_hess_far's LDS; any other
-// octave stays on k_hessian.
-static void make_far_plan_w(const FrameParams& P, const OctaveParams* oct, FarPlan& F, int strip)
-{
-    F = FarPlan{};
-    F.strip = strip;
-    static const int lobes[3][3] = {{31, 39, 47}, {63, 79, 95}, {127, 159, 191}};
-    int nfar = 0, hmax = 0, na = 0;
-    for (int o = 2; o < P.noct && nfar < farc::MAXO; o++) {
-        const OctaveParams& q = oct[o];
-        bool ok = P.sampling == 2 && q.delta == (8 << nfar) && q.nscale == 3 && q.init_scale == 2;
-        for (int i = 0; ok && i < 3; i++)
-            ok = q.mask[i] == lobes[nfar][i] && q.x2[i] == q.mask[i] / 2 && q.x3[i] == 2 * (q.mask[i] / 2) &&
-                 q.x4[i] == 3 * (q.mask[i] / 2);
-        if (!ok) break;
-        int drmin = 1 << 30, drmax = -(1 << 30);
-        for (int i = 0; i < 3; i++) {
-            HCorner t[32];
-            const int k = hessian_corners(q.mask[i], q.x2[i], q.x3[i], q.x4[i], t);
-            for (int j = 0; j < k; j++) {
-                hmax = std::max(hmax, std::abs(t[j].dc));
-                drmin = std::min(drmin, t[j].dr);
-                drmax = std::max(drmax, t[j].dr);
-            }
-        }
-        FarOct& fo = F.oc[nfar];
-        fo.o = o;
-        fo.d = q.delta;
-        fo.nS = strip / q.delta;
-        fo.drmax = drmax;
-        // sample rows in flight: a row's slot is reused NA rows later, which
-        // must start after the step that finalises it has ended
-        na = std::max(na, (drmax - drmin + farc::R - 1) / q.delta + 1);
-        nfar++;
-    }
-    if (nfar == 0) return;
-    if (na > farc::NA) return;
-    F.H = hmax <= 144 ? 144 : 288;                       // the two compiled halos
-    if (strip == farc::STRIP_W && F.H != 144) return;    // not compiled (and beyond LDS)
-    int acc = 0;
-    for (int i = 0; i < nfar; i++) {
-        F.oc[i].accoff = acc;
-        acc += farc::NA * 9 * F.oc[i].nS;
-    }
-    F.acc_total = acc;
-    const int PL = (strip + 2 * F.H) / 8;
-    F.lds_bytes = (farc::R * 8 * PL + acc) * 4;
-    if (F.lds_bytes > 160 * 1024) return;
-    int last = 0;
-    for (int i = 0; i < nfar; i++)
-        last = std::max(last, F.oc[i].d * (oct[F.oc[i].o].sh - 1) + F.oc[i].drmax);
-    F.nsteps = (last + 1 + farc::R - 1) / farc::R;
-    F.nsteps += F.nsteps & 1;                            // the loop runs steps in pairs
-    F.nstrips = (P.W + 1 + strip - 1) / strip;
-    F.nfar = nfar;
-}
-
-// The wide strip (512 columns: octave 2's samples fill a wave) where its
-// accumulators fit LDS (4 octaves: 136 KiB, one workgroup per CU), else 256
-// (5 octaves).  SURFHIP_FAR_STRIP=256 forces the narrow one (A/B).
-static void make_far_plan(const FrameParams& P, const OctaveParams* oct, FarPlan& F)
-{
-    const char* e = getenv("SURFHIP_FAR_STRIP");
-    if (!(e && atoi(e) == farc::STRIP_N)) {
-        make_far_plan_w(P, oct, F, farc::STRIP_W);
-        if (F.nfar > 0) return;
-    }
-    make_far_plan_w(P, oct, F, farc::STRIP_N);
-}
-
-// Octave o (2 or 3) of the default geometry (sampling 2: delta 8 / 16, lobes
-// 31/39/47, 63/79/95) goes to k_hess_vfar.
-static bool vfar_ok(const FrameParams& P, const OctaveParams& q, int o)
-{
-    const int d = 2 << o;
-    if (P.sampling != 2 || q.delta != d || q.nscale != 3 || q.init_scale != 2) return false;
-    for (int i = 0; i < 3; i++) {
-        const int X2 = (4 + i) * d / 2 - 1;
-        if (q.mask[i] != 2 * X2 + 1 || q.x2[i] != X2 || q.x3[i] != 2 * X2 || q.x4[i] != 3 * X2) return false;
-    }
     return true;
 }
 
@@ -1014,50 +568,37 @@ static int hw_octaves(const FrameParams& P, const OctaveParams* oct)
     return n >= 2 ? n : 0;
 }
 
-void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, FarPlan& far, int max_batch)
+// Which kernel computes each octave's planes:
+//   octave 0      k_hess_q0 (u8 frame; default geometry, batches > kGatherBatch)
+//   octaves 1-3   k_hess_w (u8 frame; default geometry, 3+ octaves)
+//   octave 1      k_hess_q1 when k_hess_w is off (2 octaves, or SURFHIP_HESS_W=0);
+//                 k_hess_q0 + k_hess_q1 in one launch (k_hess_q01) unless SURFHIP_Q01=0
+//   the rest      k_hessian, one thread per sample over the integral image
+//                 (every octave for batches <= kGatherBatch or SURFHIP_HESS_GATHER=1)
+void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, int max_batch)
 {
+    plan = LaunchPlan{};
     int hb = 0, nb = 0;
     const char* ge = getenv("SURFHIP_HESS_GATHER");
     const bool gather = ge ? atoi(ge) != 0 : max_batch <= kGatherBatch;
-    // octaves 1-3 on k_hess_w (default); SURFHIP_HESS_W=0 keeps k_hess_q1 + k_hess_far (A/B)
     const char* we = getenv("SURFHIP_HESS_W");
     plan.hw_n = (!gather && !(we && atoi(we) == 0)) ? hw_octaves(P, oct) : 0;
     plan.hw_nstrips = (P.W + hw::ST - 1) / hw::ST;
     plan.hw_nblk = ((P.H / 4 + 1 + hw::U - 1) / hw::U) * hw::U;
-    // k_hess_vfar (u8, 0.45 + 0.76 ms/batch for octaves 2 / 3) loses to the
-    // integral-image LDS kernel k_hess_far (1.03 ms for both) for now: opt-in
-    const bool use_vfar = getenv("SURFHIP_FAR_V") != nullptr;
-    plan.vfar_n = 0;
-    for (int o = 2; use_vfar && o < P.noct && o < 4 && vfar_ok(P, oct[o], o); o++) plan.vfar_n = o - 1;
-    if (plan.vfar_n > 0 || gather || plan.hw_n > 0) far = FarPlan{};   // octaves > hw_n: k_hessian
-    else make_far_plan(P, oct, far);
-    if (gather) plan.vfar_n = 0;
-    plan.o0_lds = !gather && P.noct > 0 && o0_lds_ok(P, oct[0]);
-    plan.o0_nbx = (oct[0].sw + o0::TXS - 1) / o0::TXS;     // strips per frame
-    plan.o0_blocks = plan.o0_nbx;
-    plan.o0_v = plan.o0_lds && getenv("SURFHIP_O0_RING") == nullptr;   // A/B switch back to k_hess_o0
-    // octave-0 kernel: default k_hess_q0<4, 1, 2> (packed fp32 box sums); SURFHIP_V0_SPLIT=0
-    // selects k_hess_v0 (integer accumulators) as the A/B reference
-    plan.o0_split = getenv("SURFHIP_V0_SPLIT") ? atoi(getenv("SURFHIP_V0_SPLIT")) : 44;
-    plan.o0_vstrips = (oct[0].sw + 63) / 64;
-    plan.o1_lds = !gather && P.noct > 1 && o1_lds_ok(P, oct[1]) && plan.hw_n == 0;
-    plan.o1_v = plan.o1_lds && getenv("SURFHIP_O1_RING") == nullptr;   // A/B switch back to k_hess_o1
-    // octave-1 kernel: default k_hess_q1 (packed fp32); SURFHIP_Q1=0 selects k_hess_v1
-    plan.o1_q = getenv("SURFHIP_Q1") ? atoi(getenv("SURFHIP_Q1")) != 0 : 1;
-    plan.o1_vstrips = P.noct > 1 ? (oct[1].sw + 63) / 64 : 0;
-    // octaves 0 and 1 in one launch (k_hess_q01); SURFHIP_Q01=0 launches them apart
-    plan.o01 = getenv("SURFHIP_Q01") ? atoi(getenv("SURFHIP_Q01")) != 0 : 1;
-    plan.o1_nbx = P.noct > 1 ? (oct[1].sw + o1::TXS - 1) / o1::TXS : 0;
+    plan.q0 = !gather && P.noct > 0 && q0_ok(P, oct[0]);
+    plan.q0_strips = (oct[0].sw + 63) / 64;
+    plan.q1 = !gather && P.noct > 1 && plan.hw_n == 0 && q1_ok(P, oct[1]);
+    plan.q1_strips = P.noct > 1 ? (oct[1].sw + 63) / 64 : 0;
+    const char* me = getenv("SURFHIP_Q01");
+    plan.q01 = plan.q0 && plan.q1 && !(me && atoi(me) == 0);
     for (int o = 0; o < kMaxOct; o++) {
         plan.hess_start[o] = hb;
         plan.nms_start[o] = nb;
         if (o < P.noct) {
             const OctaveParams& q = oct[o];
             plan.hess_nbx[o] = (q.sw + 63) / 64;
-            const bool on_far = o >= 2 && o < 2 + (plan.vfar_n > 0 ? plan.vfar_n : far.nfar);
-            const bool on_w = o >= 1 && o <= plan.hw_n;
-            if (!(o == 0 && plan.o0_lds) && !(o == 1 && plan.o1_lds) && !on_far && !on_w)
-                hb += plan.hess_nbx[o] * ((q.sh + 3) / 4);
+            const bool on_u8 = (o == 0 && plan.q0) || (o == 1 && plan.q1) || (o >= 1 && o <= plan.hw_n);
+            if (!on_u8) hb += plan.hess_nbx[o] * ((q.sh + 3) / 4);
             plan.nms_nbx[o] = (q.nms_gx + 63) / 64;
             plan.nms_nby[o] = (q.nms_gy + kScanRows - 1) / kScanRows;
             nb += ((P.max_scale - 1) / 2) * plan.nms_nbx[o] * plan.nms_nby[o];   // levels k = 1, 3, .. < max_scale - 1
@@ -1069,7 +610,7 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
     plan.nms_start[kMaxOct] = nb;
 }
 
-std::string hessian_plan_text(const LaunchPlan& plan, const FarPlan& far, const FrameParams& P)
+std::string hessian_plan_text(const LaunchPlan& plan, const FrameParams& P)
 {
     std::string t;
     auto add = [&](const char* k, int o0, int o1) {
@@ -1079,21 +620,13 @@ std::string hessian_plan_text(const LaunchPlan& plan, const FarPlan& far, const 
         t += o0 == o1 ? " (octave " + std::to_string(o0) + ")"
                       : " (octaves " + std::to_string(o0) + "-" + std::to_string(o1) + ")";
     };
-    if (P.noct > 0) {
-        if (plan.o01 && plan.o0_v && plan.o0_split != 0 && P.noct > 1 && plan.o1_v && plan.o1_q) {
-            add("k_hess_q01", 0, 1);
-        } else if (plan.o0_v) {
-            add(plan.o0_split == 0 ? "k_hess_v0" : "k_hess_q0", 0, 0);
-        } else if (plan.o0_lds)
-            add("k_hess_o0", 0, 0);
-    }
-    if (P.noct > 1 && !(plan.o01 && plan.o0_v && plan.o0_split != 0 && plan.o1_v && plan.o1_q)) {
-        if (plan.o1_v) add(plan.o1_q ? "k_hess_q1" : "k_hess_v1", 1, 1);
-        else if (plan.o1_lds) add("k_hess_o1", 1, 1);
+    if (plan.q01) {
+        add("k_hess_q01", 0, 1);
+    } else {
+        if (plan.q0) add("k_hess_q0", 0, 0);
+        if (plan.q1) add("k_hess_q1", 1, 1);
     }
     if (plan.hw_n > 0) add("k_hess_w", 1, plan.hw_n);
-    if (plan.vfar_n > 0) add("k_hess_vfar", 2, 1 + plan.vfar_n);
-    if (far.nfar > 0) add("k_hess_far", far.oc[0].o, far.oc[far.nfar - 1].o);
     if (plan.hess_start[kMaxOct] > 0) {
         int lo = -1, hi = -1;
         for (int o = 0; o < P.noct; o++)
@@ -1161,325 +694,39 @@ __global__ __launch_bounds__(256) void k_hessian(const int32_t* __restrict__ ii,
     }
 }
 
-// ----------------------------------------------------------------------
-// Octaves >= 2 (delta 8, 16, 32): streaming accumulation.  A sample's 32
-// corners per scale span 142 (octave 2) to 574 (octave 4) image rows, more
-// than an LDS ring can hold, and gathering them per sample touches a cache
-// line per lane.  Instead a workgroup walks a 512-column strip of one frame
-// top to bottom, reading each integral row once (coalesced) into an LDS row
-// stored as 8 residue planes (column mod 8), and every corner on that row
-// adds its weighted value into the int32 sums (dxx, dyy, dxy per scale) of
-// its sample, kept in LDS.  The sums are exact mod 2^32 and order-free, i.e.
-// identical to the reference's int arithmetic (getHessian,
-// surfd.cu:353-366); a sample row is finalised (float math in the
-// reference's order, surfd.cu:480) once its last corner row has passed.
-// Row Y carries only the corner groups of class Y mod delta, unrolled per
-// class in surfhip_far.inc (tools/gen_far.py), so every corner read is an
-// LDS immediate offset from the lane's base.
-// A step is R = 16 integral rows (SURF_FAR_R; one wave per ring row, 1024
-// threads); the step's corner groups are dealt to the waves by cost
-// (gen_far.py), and wave w finalises (octave, scale) unit w (unit = 3 octave
-// + scale), up to R / delta sample rows per step.  The ring holds one step;
-// its rows were loaded into registers two steps earlier.  512-column strips
-// (octave 2's samples fill a wave) take 134 KiB of LDS: one 16-wave
-// workgroup per CU.  The strips of a frame run on one XCD, so the column
-// halo comes from L2 (HBM reads = one integral image per frame, FETCH_SIZE).
-// LDS: ring[R][8 planes][PL] | acc (per octave [NA][9][nS]).
-// ----------------------------------------------------------------------
-#include "surfhip_far.inc"
-
-template <int NI, int H, int ST>
-__device__ __forceinline__ void far_load(uint4 (&dst)[NI], rsrc_t I, int ip, int iH, int cs, int Y0)
-{
-    constexpr int NC4 = (ST + 2 * H) / 4;
-#pragma unroll
-    for (int i = 0; i < NI; i++) {
-        const int t = (int)threadIdx.x + i * farc::THREADS;
-        const int r = t / NC4, q = t - r * NC4;
-        const int gy = Y0 + r;
-        const bool ok = r < farc::R && gy < iH;
-#ifdef SURF_DIAG_FAR_NOLOAD
-        dst[i] = make_uint4((uint32_t)gy, (uint32_t)q, (uint32_t)cs, (uint32_t)ip);
-        (void)ok;
-#else
-        dst[i] = buf_ld4(I, ok ? (uint32_t)(gy * ip + cs + 4 * q) * 4u : kOOB);
-#endif
-    }
-}
-
-// columns 4q .. 4q + 3 of a row go to planes (4q & 7) + 0..3, index q / 2
-template <int NI, int H, int ST>
-__device__ __forceinline__ void far_ring_store(const uint4 (&src)[NI], uint32_t* ring)
-{
-    constexpr int NC4 = (ST + 2 * H) / 4, PL = (ST + 2 * H) / 8;
-#pragma unroll
-    for (int i = 0; i < NI; i++) {
-        const int t = (int)threadIdx.x + i * farc::THREADS;
-        const int r = t / NC4, q = t - r * NC4;
-        if (r < farc::R) {
-            uint32_t* d = ring + (r * 8 + 4 * (q & 1)) * PL + (q >> 1);
-            d[0] = src[i].x;
-            d[PL] = src[i].y;
-            d[2 * PL] = src[i].z;
-            d[3 * PL] = src[i].w;
-        }
-    }
-}
-
-template <int NI, int H, int ST>
-__global__ __launch_bounds__(farc::THREADS) void k_hess_far(const int32_t* __restrict__ ii,
-                                                              float* __restrict__ resp, FrameParams P,
-                                                              const OctaveParams* __restrict__ oct, FarPlan F,
-                                                              int nframes)
-{
-    constexpr int PL = (ST + 2 * H) / 8;
-    constexpr int ROWW = 8 * PL;
-    static_assert(farc::THREADS == 64 * farc::R, "one wave per ring row");
-    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
-    const int xcd = blockIdx.x & 7, kb = blockIdx.x >> 3;
-    const int f = (kb / F.nstrips) * 8 + xcd, strip = kb - (kb / F.nstrips) * F.nstrips;
-    if (f >= nframes) return;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int X0 = strip * ST, cs = X0 - H;
-    const int nfar = F.nfar;
-    uint32_t* ring = sm;
-    int* acc = reinterpret_cast<int*>(sm + farc::R * ROWW);
-    for (int i = tid; i < F.acc_total; i += farc::THREADS) acc[i] = 0;
-    const rsrc_t I = make_rsrc(ii + (size_t)f * P.ii_stride, (long long)P.iH * P.ip * 4);
-    const rsrc_t Rs = make_rsrc(resp + (size_t)f * P.resp_stride, P.resp_stride * 4);
-    const int ip = P.ip, iH = P.iH;
-    const int sh2 = oct[2].sh;
-    const int sh3 = nfar > 1 ? oct[3].sh : 0, sh4 = nfar > 2 ? oct[4].sh : 0;
-    int next_iy[farc::MAXO] = {0, 0, 0};
-    // the loop-invariant parameters of this wave's two finalisation units
-    // (octave, scale) = wv and wv + 8 and of the row tracking, read once
-    // (loads from oct inside the loop are repeated after every barrier)
-    struct FinUnit {
-        bool on, colok, colin;
-        int oi, d, drmax, nS, sh, sp, b1, accoff;
-        long long pbase;
-        float norm;
-    };
-    FinUnit fu[2];
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-        const int unit = wv + farc::R * k;
-        const int fo_i = unit / 3, fo_s = unit - 3 * fo_i;
-        FinUnit& u = fu[k];
-        u.on = fo_i < nfar;
-        const FarOct& fo = F.oc[u.on ? fo_i : 0];
-        const OctaveParams& q = oct[fo.o];
-        u.oi = u.on ? fo_i : 0;
-        u.d = fo.d;
-        u.drmax = fo.drmax;
-        u.nS = fo.nS;
-        u.sh = q.sh;
-        u.sp = q.sp;
-        u.b1 = q.b1[fo_s];
-        u.norm = q.norm[fo_s];
-        u.accoff = fo.accoff + 3 * fo_s * fo.nS + lane;
-        u.pbase = q.ooff + (long long)(q.init_scale + fo_s) * q.osize + X0 / fo.d + lane;
-        const int ix = X0 / fo.d + lane;
-        u.colok = ix >= u.b1 && ix < q.sw - u.b1;
-        u.colin = ix < q.sw;
-    }
-    int osh[farc::MAXO], odr[farc::MAXO], odm[farc::MAXO];
-#pragma unroll
-    for (int oi = 0; oi < farc::MAXO; oi++) {
-        const FarOct& fo = F.oc[oi < nfar ? oi : 0];
-        osh[oi] = oct[fo.o].sh;
-        odr[oi] = fo.d;
-        odm[oi] = fo.drmax;
-    }
-
-    uint4 A[NI], B[NI];
-    far_load<NI, H, ST>(A, I, ip, iH, cs, 0);                         // rows of step 0
-    far_load<NI, H, ST>(B, I, ip, iH, cs, farc::R);                   // rows of step 1
-    // finalised responses of the previous step, stored at the start of the
-    // next one: every step issues its two stores before its loads, with no
-    // branch around them, so hipcc's count of outstanding VMEM ops is exact
-    // and the ring write waits only for the loads of two steps back
-    // MR: sample rows a unit may finalise per step (R / delta, delta >= 8)
-    constexpr int MR = farc::R / 8;
-    uint32_t poff[2][MR];
-    float ph[2][MR];
-#pragma unroll
-    for (int k = 0; k < 2; k++)
-#pragma unroll
-        for (int m = 0; m < MR; m++) { poff[k][m] = kOOB; ph[k][m] = 0.f; }
-
-    // One step: rows Y0 .. Y0 + R - 1.  `cur` (this step's rows, loaded two
-    // steps earlier) goes to the ring, then `cur` receives the loads for
-    // step s + 2.
-    auto step = [&](int sidx, uint4 (&cur)[NI]) {
-        const int Y0 = sidx * farc::R;
-        far_ring_store<NI, H, ST>(cur, ring);
-#pragma unroll
-        for (int k = 0; k < 2; k++)
-#pragma unroll
-            for (int m = 0; m < MR; m++) buf_st_nt(Rs, poff[k][m], ph[k][m]);
-        far_load<NI, H, ST>(cur, I, ip, iH, cs, Y0 + 2 * farc::R);
-        __syncthreads();
-        // ---- accumulate every corner on the step's rows
-        {
-            // the step's corner groups of every far octave, dealt to the R
-            // waves by cost (tools/gen_far.py, emit_balanced)
-#ifndef SURF_DIAG_FAR_NOACC
-            far_bal<H, PL, ROWW, ST>(nfar, sidx, wv, ring, lane, acc + F.oc[0].accoff + lane,
-                                     acc + F.oc[1].accoff + lane, acc + F.oc[2].accoff + lane, Y0 >> 3, Y0 >> 4,
-                                     Y0 >> 5, sh2, sh3, sh4, (int)((unsigned)(Y0 >> 3) % farc::NA),
-                                     (int)((unsigned)(Y0 >> 4) % farc::NA), (int)((unsigned)(Y0 >> 5) % farc::NA));
-#endif
-        }
-        __syncthreads();
-        // ---- finalise the sample rows (of each far octave) whose last corner
-        // row has passed: at most R / delta per octave per step; wave w takes
-        // units (octave, scale) w and w + R
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-            const FinUnit& u = fu[k];
-#pragma unroll
-            for (int m = 0; m < MR; m++) {
-                uint32_t off = kOOB;
-                float h = 0.f;
-                if (u.on) {
-                    const int iy = next_iy[u.oi] + m;
-                    if (iy < u.sh && u.d * iy + u.drmax <= Y0 + farc::R - 1 && lane < u.nS) {
-                        int* a = acc + u.accoff + ((unsigned)iy % farc::NA) * 9 * u.nS;
-                        const int32_t sxx = a[0], syy = a[u.nS], sxy = a[2 * u.nS];
-                        a[0] = 0;
-                        a[u.nS] = 0;
-                        a[2 * u.nS] = 0;
-                        const float rr = INV255 * INV255;
-                        const float dxx = (float)sxx;
-                        const float dyy = (float)syy;
-                        const float dxy = 0.6f * (float)sxy;
-                        const float pp = dxx * dyy;
-                        const float q2 = dxy * dxy;
-                        const bool v = iy >= u.b1 && iy < u.sh - u.b1 && u.colok;
-                        h = v ? (rr * (pp - q2)) * u.norm : 0.f;
-                        if (u.colin) off = (uint32_t)(u.pbase + iy * u.sp) * 4u;
-                    }
-                }
-                poff[k][m] = off;
-                ph[k][m] = h;
-            }
-        }
-        // every wave tracks every octave's next row identically
-#pragma unroll
-        for (int oi = 0; oi < farc::MAXO; oi++) {
-#pragma unroll
-            for (int m = 0; m < MR; m++)
-                if (oi < nfar && next_iy[oi] < osh[oi] && odr[oi] * next_iy[oi] + odm[oi] <= Y0 + farc::R - 1)
-                    next_iy[oi]++;
-        }
-        // no barrier here: the next step's ring writes come after every wave
-        // passed this step's second barrier (all reads of the ring done), and
-        // the accumulator slots zeroed above are not reused for NA rows
-    };
-    for (int s2 = 0; s2 < F.nsteps; s2 += 2) {
-        step(s2, A);
-        step(s2 + 1, B);
-    }
-#pragma unroll
-    for (int k = 0; k < 2; k++)
-#pragma unroll
-        for (int m = 0; m < MR; m++) buf_st_nt(Rs, poff[k][m], ph[k][m]);
-}
-
-template <int H, int ST>
-static hipError_t launch_far(const int32_t* ii, float* resp, int nframes, const FrameParams& P,
-                             const OctaveParams* d_oct, const FarPlan& far, hipStream_t s)
-{
-    // rows of a step = R x (ST + 2H) columns in uint4 items, NI per thread
-    constexpr int NI = (farc::R * (ST + 2 * H) / 4 + farc::THREADS - 1) / farc::THREADS;
-    hipError_t e = set_max_lds(reinterpret_cast<const void*>(&k_hess_far<NI, H, ST>), 160 * 1024);
-    if (e != hipSuccess) return e;
-    const int nf8 = (nframes + 7) & ~7;
-    k_hess_far<NI, H, ST><<<dim3(nf8 * far.nstrips), farc::THREADS, far.lds_bytes, s>>>(ii, resp, P, d_oct, far, nframes);
-    return hipSuccess;
-}
-
 hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, const int32_t* ii, float* resp,
                           int nframes, const FrameParams& P, const OctaveParams* d_oct, const OctaveParams* h_oct,
-                          const LaunchPlan& plan, const FarPlan& far, hipStream_t s, int parts)
+                          const LaunchPlan& plan, hipStream_t s, int parts)
 {
     const int nf8 = (nframes + 7) & ~7;
     // parts: 1 = the kernels that read the u8 frames, 2 = those that read the
     // integral image (the two may run on different streams)
-    if (!frames) parts = 3;
     const bool u8p = (parts & 1) != 0, iip = (parts & 2) != 0;
-    const bool merged = plan.o01 && plan.o0_v && plan.o0_split != 0 && plan.o1_v && plan.o1_q && frames;
-    if (merged && u8p) {
-        const int nb0 = 8 * (((nf8 / 8) * plan.o0_vstrips + q0::WAVES - 1) / q0::WAVES);
-        const int nb1 = 8 * (((nf8 / 8) * plan.o1_vstrips + q1::WAVES - 1) / q1::WAVES);
-        k_hess_q01<<<dim3(nb0 + nb1), q0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0], h_oct[1],
-                                                           plan.o0_vstrips, plan.o1_vstrips, nb0, nframes);
-    }
-    if (merged) {
-    } else if (plan.o0_v && frames) {
-        if (u8p) {
-        const int per_xcd = (nf8 / 8) * plan.o0_vstrips;           // wave tasks per XCD
-        const dim3 g(8 * ((per_xcd + v0::WAVES - 1) / v0::WAVES));
-        if (plan.o0_split == 0) {       // A/B: the integer-accumulator kernel of round 1
-            k_hess_v0<4, 1, 0x1f><<<g, v0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
-                                                            plan.o0_vstrips, nframes);
-        } else {                        // default: packed fp32 box sums, rebased local integral
-            const dim3 gq(8 * ((per_xcd + q0::WAVES - 1) / q0::WAVES));
-            k_hess_q0<4, 1, 2><<<gq, q0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
-                                                          plan.o0_vstrips, nframes);
+    if (u8p && !frames && (plan.q0 || plan.q1 || plan.hw_n > 0)) return hipErrorInvalidValue;
+    if (u8p) {
+        const int nb0 = 8 * (((nf8 / 8) * plan.q0_strips + q0::WAVES - 1) / q0::WAVES);
+        const int nb1 = 8 * (((nf8 / 8) * plan.q1_strips + q1::WAVES - 1) / q1::WAVES);
+        if (plan.q01) {
+            k_hess_q01<<<dim3(nb0 + nb1), q0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0], h_oct[1],
+                                                               plan.q0_strips, plan.q1_strips, nb0, nframes);
+        } else {
+            if (plan.q0)
+                k_hess_q0<4, 1, 2><<<dim3(nb0), q0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
+                                                                     plan.q0_strips, nframes);
+            if (plan.q1)
+                k_hess_q1<2><<<dim3(nb1), q1::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[1],
+                                                               plan.q1_strips, nframes);
         }
-        }
-    } else if (plan.o0_lds && iip)
-        k_hess_o0<<<dim3(nf8 * plan.o0_nbx), o0::THREADS, 0, s>>>(ii, resp, P, h_oct[0], plan.o0_nbx, nframes);
-    if (merged) {
-    } else if (plan.o1_v && frames) {
-        if (u8p) {
-        const int per_xcd = (nf8 / 8) * plan.o1_vstrips;
-        if (plan.o1_q)
-            k_hess_q1<2><<<dim3(8 * ((per_xcd + q1::WAVES - 1) / q1::WAVES)), q1::THREADS, 0, s>>>(
-                frames, pitch, fstride, resp, P, h_oct[1], plan.o1_vstrips, nframes);
-        else
-            k_hess_v1<<<dim3(8 * ((per_xcd + v1::WAVES - 1) / v1::WAVES)), v1::THREADS, 0, s>>>(
-                frames, pitch, fstride, resp, P, h_oct[1], plan.o1_vstrips, nframes);
-        }
-    } else if (plan.o1_lds && iip)
-        k_hess_o1<<<dim3(nf8 * plan.o1_nbx), o1::THREADS, 0, s>>>(ii, resp, P, h_oct[1], plan.o1_nbx, nframes);
-    if (plan.hw_n > 0 && frames && u8p) {
-        const dim3 g(nf8 * plan.hw_nstrips);
-        const OctaveParams& q3 = h_oct[plan.hw_n >= 3 ? 3 : 2];
-        if (plan.hw_n >= 3)
-            k_hess_w<3><<<g, hw::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[1], h_oct[2], q3,
-                                                  plan.hw_nstrips, nframes, plan.hw_nblk);
-        else
-            k_hess_w<2><<<g, hw::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[1], h_oct[2], q3,
-                                                  plan.hw_nstrips, nframes, plan.hw_nblk);
-    }
-    if (plan.vfar_n > 0 && frames && u8p) {
-        // octave 2: 3 vertical segments, octave 3: 2 (parallelism); one launch each
-        for (int o = 2; o < 2 + plan.vfar_n; o++) {
-            const OctaveParams& q = h_oct[o];
-            const int nstrips = (q.sw + 63) / 64;
-            const int nseg = o == 2 ? 3 : 2;
-            const int segrows = (q.sh + nseg - 1) / nseg;
-            const int per_xcd = (nf8 / 8) * nstrips * nseg;
-            if (o == 2)
-                k_hess_vfar<8, 16, 8, 4, 4><<<dim3(8 * ((per_xcd + 3) / 4)), 256, 0, s>>>(
-                    frames, pitch, fstride, resp, P, q, nstrips, nseg, segrows, nframes);
+        if (plan.hw_n > 0) {
+            const dim3 g(nf8 * plan.hw_nstrips);
+            const OctaveParams& q3 = h_oct[plan.hw_n >= 3 ? 3 : 2];
+            if (plan.hw_n >= 3)
+                k_hess_w<3><<<g, hw::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[1], h_oct[2], q3,
+                                                      plan.hw_nstrips, nframes, plan.hw_nblk);
             else
-                k_hess_vfar<16, 32, 4, 4, 2><<<dim3(8 * ((per_xcd + 1) / 2)), 128, 0, s>>>(
-                    frames, pitch, fstride, resp, P, q, nstrips, nseg, segrows, nframes);
+                k_hess_w<2><<<g, hw::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[1], h_oct[2], q3,
+                                                      plan.hw_nstrips, nframes, plan.hw_nblk);
         }
-    }
-    if (far.nfar > 0 && iip) {
-        // rows of a step = R x (STRIP + 2H) columns in uint4 items: 1088 (H 144) / 1664 (H 288)
-        // (the wide strip only with the 144 halo: make_far_plan_w)
-        const hipError_t e = far.strip == farc::STRIP_W ? launch_far<144, farc::STRIP_W>(ii, resp, nframes, P, d_oct, far, s)
-                             : far.H == 144             ? launch_far<144, farc::STRIP_N>(ii, resp, nframes, P, d_oct, far, s)
-                                                        : launch_far<288, farc::STRIP_N>(ii, resp, nframes, P, d_oct, far, s);
-        if (e != hipSuccess) return e;
     }
     if (plan.hess_start[kMaxOct] > 0 && iip)
         k_hessian<<<dim3(frame_grid(nframes) * plan.hess_start[kMaxOct]), 256, 0, s>>>(ii, resp, P, d_oct, plan,

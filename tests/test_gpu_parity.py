@@ -149,7 +149,7 @@ def _extreme_frame(kind, w, h, pitch):
 
 
 @pytest.mark.parametrize("kind", ["white", "noise", "vstripes", "checker", "hbands", "vbands"])
-@pytest.mark.parametrize("env", ["SURFHIP_V0_SPLIT=44", "SURFHIP_V0_SPLIT=0", "SURFHIP_Q1=0"])
+@pytest.mark.parametrize("env", ["SURFHIP_HESS_W=1", "SURFHIP_HESS_W=0"])
 def test_hessian_planes_extreme_frames(surf, orc, monkeypatch, kind, env):
     w, h = 1920, 1080
     name, _, val = env.partition("=")
@@ -165,16 +165,17 @@ def test_hessian_planes_extreme_frames(surf, orc, monkeypatch, kind, env):
         assert same.all(), f"{kind}/{env}: octave {o} scale {s}: {(~same).sum()} cells differ"
 
 
-@pytest.mark.parametrize("env", ["SURFHIP_O0_RING", "SURFHIP_O1_RING", "SURFHIP_FAR_V", "SURFHIP_V0_SPLIT=0",
-                                 "SURFHIP_V0_SPLIT=44", "SURFHIP_Q1=0", "SURFHIP_Q1=1", "SURFHIP_Q01=0", "SURFHIP_FAR_STRIP=256",
-                                 "SURFHIP_HESS_GATHER=1"])
-@pytest.mark.parametrize("w,h,noct", [(640, 480, 4), (1920, 1080, 4)])
+@pytest.mark.parametrize("env", ["SURFHIP_HESS_W=0", "SURFHIP_HESS_W=0,SURFHIP_Q01=0", "SURFHIP_HESS_GATHER=1"])
+@pytest.mark.parametrize("w,h,noct", [(640, 480, 4), (1920, 1080, 4), (1920, 1080, 2), (960, 540, 3)])
 def test_hessian_alternate_kernels_bit_exact(surf, orc, monkeypatch, env, w, h, noct):
-    """The selectable Hessian kernels (integral-image rings for octaves 0/1,
-    the u8 vertical-streaming kernel for octaves 2/3) give the same planes;
-    the plan reads these switches when a detector is created."""
-    name, _, val = env.partition("=")
-    monkeypatch.setenv(name, val or "1")
+    """The selectable Hessian plans give the same planes: k_hess_q1 (alone or
+    merged with k_hess_q0 in k_hess_q01) + the gather kernel instead of
+    k_hess_w, and the all-gather plan; 2 octaves (no k_hess_w) and 3 octaves
+    (k_hess_w with octaves 1-2).  The plan reads these switches when a
+    detector is created."""
+    for kv in env.split(","):
+        name, _, val = kv.partition("=")
+        monkeypatch.setenv(name, val or "1")
     frames = surf.synth_frames(1, w, h, first=21)
     param = surf.make_param(noct, 4.0, upright=True)
     res = gpu_run(surf, param, frames, w, h, want_ws=True, desc=False)
