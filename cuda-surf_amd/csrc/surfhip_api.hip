@@ -332,11 +332,17 @@ static int derive(surfhip_detector* d)
             borders[0] = border1;
             borders[1] = border1;
             s = 2;
-            q.psp = d->oct[o - 1].sp;
-            q.posize = d->oct[o - 1].osize;
-            q.pooff = d->oct[o - 1].ooff;
-            q.half[0] = p.max_scale - 3;
-            q.half[1] = p.max_scale - 1;
+            for (int t = 0; t < 2; t++) {
+                int pl = t == 0 ? p.max_scale - 3 : p.max_scale - 1, oo = o - 1, st = 2;
+                while (pl < 2 && oo > 0) {      // a copy of a copy (4 scales per octave)
+                    pl = pl == 0 ? p.max_scale - 3 : p.max_scale - 1;
+                    oo--;
+                    st *= 2;
+                }
+                q.hbase[t] = d->oct[oo].ooff + (long long)pl * d->oct[oo].osize;
+                q.hrow[t] = d->oct[oo].sp * st;
+                q.hcol[t] = st;
+            }
         } else {
             border1 = ((3 * (mask_size + 6 * octave)) / 2) / (p.sampling * octave) + 1;
             s = 0;

@@ -50,11 +50,14 @@ struct OctaveParams {
     int borders[kMaxScale];         // host borders[] (d_borders), index s
     int mb[(kMaxScale - 2) / 2];    // NMS start offsets (maximum_borders, one per level)
     int nms_gx, nms_gy;             // NMS launch extent in threads
-    // previous octave (source of the halfImage planes 0 and 1: its planes
-    // max_scale - 3 and max_scale - 1, surf.cpp:252-258)
-    int psp, posize;
-    long long pooff;
-    int half[2];
+    // planes 0 and 1 of an octave > 0 are the reference's halfImage copies of
+    // the previous octave's planes max_scale - 3 / max_scale - 1
+    // (surf.cpp:252-258), never materialised: read in place at (r, c) ->
+    // hbase[t] + r * hrow[t] + c * hcol[t] (floats).  With 4 scales plane
+    // max_scale - 3 = 1 is itself a copy, so the chain is followed back to a
+    // computed plane (stride 4, 8, ..).
+    long long hbase[2];
+    int hrow[2], hcol[2];
 };
 
 // Frame-level parameters (SurfParam + integral geometry).

@@ -776,26 +776,31 @@ __device__ void solve3(float* sol, float (&sq)[3][3])
 // o-1's planes 2/4 at (2r, 2c), which is exactly what halfImage copied.
 struct OctView {
     const float* F;                 // the frame's response block
-    int cur, prev;                  // float offsets of this octave's / the previous octave's plane 0 (-1: none)
-    int sp, osize, psp, posize;
-    int h0, h1;                     // halfImage sources: planes max_scale - 3 / - 1 of the previous octave
+    int cur;                        // float offset of this octave's plane 0
+    int sp, osize;
+    int half;                       // octave > 0: planes 0 / 1 are the halfImage views
+    // plane 0's view and plane 1's differences from it (a select against a
+    // constant: selecting between two fields became a select of their
+    // addresses and put the view in scratch)
+    int hb, hr, hc, dhb, dhr, dhc;
     // branch-free (selects): a branch around a load makes hipcc wait for the
     // loads issued before it at the join, which serialised the NMS scan's 32
     // block loads into 16 memory round trips
     __device__ __forceinline__ int off(int s, int r, int c) const
     {
-        const bool h = prev >= 0 && s < 2;          // planes 0/1 of octave > 0: previous octave, 2x stride
-        const int base = h ? prev + (s == 0 ? h0 : h1) * posize : cur + s * osize;
-        return base + r * (h ? 2 * psp : sp) + (h ? 2 * c : c);
+        const bool h = half && s < 2;
+        const bool p1 = s != 0;
+        const int base = h ? hb + (p1 ? dhb : 0) : cur + s * osize;
+        return base + r * (h ? hr + (p1 ? dhr : 0) : sp) + c * (h ? hc + (p1 ? dhc : 0) : 1);
     }
     __device__ __forceinline__ float operator()(int s, int r, int c) const { return F[off(s, r, c)]; }
     // (s, r, c) and (s, r, c + 1)
     __device__ __forceinline__ void pair(int s, int r, int c, float& a, float& b) const
     {
-        const bool h = prev >= 0 && s < 2;
+        const bool h = half && s < 2;
         const int o = off(s, r, c);
         a = F[o];
-        b = F[o + (h ? 2 : 1)];
+        b = F[o + (h ? hc + (s != 0 ? dhc : 0) : 1)];
     }
 };
 
@@ -942,13 +947,15 @@ __device__ __forceinline__ OctView make_view(const float* F, const OctaveParams&
     OctView V;
     V.F = F;
     V.cur = (int)q.ooff;
-    V.prev = o > 0 ? (int)q.pooff : -1;
     V.sp = q.sp;
     V.osize = q.osize;
-    V.psp = q.psp;
-    V.posize = q.posize;
-    V.h0 = q.half[0];
-    V.h1 = q.half[1];
+    V.half = o > 0 ? 1 : 0;
+    V.hb = (int)q.hbase[0];
+    V.dhb = (int)(q.hbase[1] - q.hbase[0]);
+    V.hr = q.hrow[0];
+    V.dhr = q.hrow[1] - q.hrow[0];
+    V.hc = q.hcol[0];
+    V.dhc = q.hcol[1] - q.hcol[0];
     return V;
 }
 
@@ -1126,17 +1133,20 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
                         i_r_c = V(si, r, c); i_r_cm = V(si, r, c - dc); i_rp_c = V(si, rp, c);
                     }
                     // V(s + a, r + b, c + e) for the positions fit_quad reads
+                    // (selects, not indexing: nb stays in registers)
+                    auto pick = [](int e, float m, float z, float p) -> float { return e < 0 ? m : (e == 0 ? z : p); };
                     auto so_at = [&](int b, int e) -> float {
-                        return b == 0 ? nb[4 + e] : (b == dr ? nb[7 + e] : nb[1 + e]);
+                        return b == 0 ? pick(e, nb[3], nb[4], nb[5])
+                                      : (b == dr ? pick(e, nb[6], nb[7], nb[8]) : pick(e, nb[0], nb[1], nb[2]));
                     };
                     auto s_at = [&](int b, int e) -> float {
                         if (b == 0) return e == 0 ? best : (e == dc ? nb[12] : b_r_cm);
-                        if (b == dr) return nb[10 + e];
+                        if (b == dr) return pick(e, nb[9], nb[10], nb[11]);
                         return e == 0 ? b_rp_c : (e == dc ? nb[13] : b_rp_cm);
                     };
                     auto si_at = [&](int b, int e) -> float {       // no corner is read
                         if (b == 0) return e == 0 ? i_r_c : (e == dc ? nb[18] : i_r_cm);
-                        if (b == dr) return nb[15 + e];
+                        if (b == dr) return pick(e, nb[14], nb[15], nb[16]);
                         return i_rp_c;
                     };
                     auto at = [&](int a, int b, int e) -> float {
