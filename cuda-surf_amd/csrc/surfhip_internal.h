@@ -90,6 +90,7 @@ struct LaunchPlan {
     int nms_start[kMaxOct + 1];     // NMS blocks of octave o (every level)
     int nms_nbx[kMaxOct], nms_nby[kMaxOct];
     int q0, q0_strips;              // octave 0 on k_hess_q0 (u8 vertical streaming), 64-sample strips
+    int p0;                         // ... on k_hess_p0 instead (producer + per-scale waves): its interval B; 0: q0
     int q1, q1_strips;              // octave 1 on k_hess_q1 (when k_hess_w is off)
     int q01;                        // q0 and q1 in one launch (k_hess_q01)
     int hw_n;                       // octaves 1 .. hw_n on k_hess_w (u8, shared strip integral); 0: off

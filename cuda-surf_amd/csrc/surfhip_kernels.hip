@@ -520,6 +520,7 @@ __device__ __forceinline__ float hessian_at(const uint32_t* __restrict__ I, int 
 
 #include "surfhip_hess_q0.inc"
 #include "surfhip_hess_q1.inc"
+#include "surfhip_hess_p0.inc"
 #include "surfhip_hess_w.inc"
 
 // Octave 1 on k_hess_q1 (only when k_hess_w is off: 2-octave detectors or
@@ -591,6 +592,13 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
     plan.q1_strips = P.noct > 1 ? (oct[1].sw + 63) / 64 : 0;
     const char* me = getenv("SURFHIP_Q01");
     plan.q01 = plan.q0 && plan.q1 && !(me && atoi(me) == 0);
+    // octave 0 on k_hess_p0 unless SURFHIP_P0=0; SURFHIP_P0=BG picks its
+    // barrier interval B (steps) and consumer waves G
+    // (value 10 B + G: barrier interval B steps, G consumer waves)
+    const char* pe = getenv("SURFHIP_P0");
+    plan.p0 = (plan.q0 && !plan.q01) ? (pe ? atoi(pe) : 93) : 0;
+    if (plan.p0 != 0 && plan.p0 != 95 && plan.p0 != 93 && plan.p0 != 92 && plan.p0 != 91 && plan.p0 != 32)
+        plan.p0 = 93;
     for (int o = 0; o < kMaxOct; o++) {
         plan.hess_start[o] = hb;
         plan.nms_start[o] = nb;
@@ -623,7 +631,8 @@ std::string hessian_plan_text(const LaunchPlan& plan, const FrameParams& P)
     if (plan.q01) {
         add("k_hess_q01", 0, 1);
     } else {
-        if (plan.q0) add("k_hess_q0", 0, 0);
+        if (plan.p0) add("k_hess_p0", 0, 0);
+        else if (plan.q0) add("k_hess_q0", 0, 0);
         if (plan.q1) add("k_hess_q1", 1, 1);
     }
     if (plan.hw_n > 0) add("k_hess_w", 1, plan.hw_n);
@@ -710,7 +719,15 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
             k_hess_q01<<<dim3(nb0 + nb1), q0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0], h_oct[1],
                                                                plan.q0_strips, plan.q1_strips, nb0, nframes);
         } else {
-            if (plan.q0)
+            const dim3 gp(nf8 * plan.q0_strips);
+            const int pb = plan.p0 / 10, pg = plan.p0 % 10;      // interval, consumer waves
+#define P0_CASE(BB, GG)                                                                                          \
+    else if (pb == BB && pg == GG) k_hess_p0<BB, GG, 1><<<gp, 64 * (1 + GG), 0, s>>>(frames, pitch, fstride, resp, P, \
+                                                                                    h_oct[0], plan.q0_strips, nframes);
+            if (false) {}
+            P0_CASE(9, 5) P0_CASE(9, 3) P0_CASE(9, 2) P0_CASE(9, 1) P0_CASE(3, 2)
+#undef P0_CASE
+            else if (plan.q0)
                 k_hess_q0<4, 1, 2><<<dim3(nb0), q0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
                                                                      plan.q0_strips, nframes);
             if (plan.q1)
