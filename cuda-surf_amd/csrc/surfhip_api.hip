@@ -255,7 +255,7 @@ int surfhip_make_param(surfhip_param* out, int noctaves, float thresh, int doubl
 {
     if (!out) return SURFHIP_ERR_INVALID;
     memset(out, 0, sizeof(*out));
-    if (noctaves < 1 || noctaves > kMaxOct || desc_wsz < 1 || 12 % desc_wsz != 0 || sampling_step < 1)
+    if (noctaves < 1 || noctaves > kMaxOct || desc_wsz < 1 || sampling_step < 1)
         return SURFHIP_ERR_INVALID;
     out->doubled = doubled != 0;
     out->noctaves = noctaves;
@@ -273,7 +273,11 @@ int surfhip_make_param(surfhip_param* out, int noctaves, float thresh, int doubl
     // scales per octave: MAX_SCALE (surfd.h:9) bounds them; below 4 the
     // octaves > 0 compute fewer than 2 scales and the lobes degenerate
     if (out->max_scale < 4 || out->max_scale > kMaxScale) return SURFHIP_ERR_UNSUPPORTED;
-    if (out->nfeatures > 128) return SURFHIP_ERR_UNSUPPORTED;
+    // a sample's Gaussian weight is lookup2[(int)(rpos^2 + cpos^2)]
+    // (surfd.cu:1303, 1335, 1999) with |rpos|, |cpos| < (desc_wsz + 1) / 2,
+    // and lookup2 has 40 entries (surfd.cu:23): from desc_wsz 8 on the
+    // reference reads past it.  desc_wsz <= 7: at most 7 x 7 x 8 = 392 features.
+    if (desc_wsz > 7) return SURFHIP_ERR_UNSUPPORTED;
     return SURFHIP_OK;
 }
 
@@ -772,7 +776,7 @@ size_t surfhip_match_scratch(int n1, int n2, int flags)
 int surfhip_match(surfhip_point* pts1, const surfhip_point* pts2, const float* f1, const float* f2, int n1, int n2,
                   int nf, int flags, void* scratch, void* stream)
 {
-    if (n1 < 0 || n2 < 0 || nf < 4 || nf > 128 || (nf & 3) || (flags & ~SURFHIP_MATCH_FULL_TAIL))
+    if (n1 < 0 || n2 < 0 || nf < 4 || nf > 1024 || (nf & 3) || (flags & ~SURFHIP_MATCH_FULL_TAIL))
         return SURFHIP_ERR_INVALID;
     if (n1 == 0) return SURFHIP_OK;
     if (!pts1 || !f1 || (n2 > 0 && (!pts2 || !f2))) return SURFHIP_ERR_INVALID;

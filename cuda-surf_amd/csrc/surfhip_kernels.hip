@@ -1859,18 +1859,20 @@ struct KpQueue {
     }
 };
 
-template <bool UPRIGHT>
+template <bool UPRIGHT, int MAXF>
 __global__ __launch_bounds__(256) void k_describe(const int32_t* __restrict__ ii, FrameParams P,
                                                   surfhip_point* __restrict__ pts, int max_pts,
                                                   const int* __restrict__ counts, const int* __restrict__ offsets,
                                                   const int* __restrict__ order, int nframes, float* __restrict__ desc,
                                                   int* __restrict__ queue)
 {
-    // four copies of the descriptor per wave (copy = lane & 3, 132-float
-    // stride so that one bin's copies sit in different banks): neighbouring
-    // samples, which mostly hit the same cell and bin, no longer serialise
-    // on one LDS address; the copies are summed before normalisation
-    constexpr int DSTR = 132;
+    // four copies of the descriptor per wave (copy = lane & 3, MAXF + 4
+    // floats apart so that one bin's copies sit in different banks):
+    // neighbouring samples, which mostly hit the same cell and bin, no longer
+    // serialise on one LDS address; the copies are summed before
+    // normalisation.  MAXF: 128, or 512 for windows past 4 x 4 x 8.
+    constexpr int DSTR = MAXF + 4;
+    constexpr int NV = MAXF / 64;                // outputs per lane
     __shared__ float sdesc[4][4 * DSTR];
     __shared__ OriScratch sori[UPRIGHT ? 1 : 4];
     const unsigned lane = lane_id();
@@ -1962,19 +1964,33 @@ __global__ __launch_bounds__(256) void k_describe(const int32_t* __restrict__ ii
             }
         }
         wave_sync();
-        // normalize (surfd.cu:2447-2493): sequential-addressing tree
+        // normalize (surfd.cu:2447-2493): the squares zero-padded to P =
+        // max(64, pow2 >= nf) in the sequential-addressing tree: strides P/2
+        // .. 64 fold lane + 64 m (m < P / 64) pairwise, then 32 .. 1 across
+        // the lanes (for nf = 64 / 128 exactly the reference's order)
         auto sum4 = [&](int b) { return ((d0[b] + d0[DSTR + b]) + d0[2 * DSTR + b]) + d0[3 * DSTR + b]; };
-        const float v0 = lane < (unsigned)nf ? sum4(lane) : 0.f;
-        const float v1 = (nf > 64 && lane + 64 < (unsigned)nf) ? sum4(lane + 64) : 0.f;
-        float a = v0 * v0;
-        if (nf > 64) a = a + v1 * v1;
+        float v[NV], a2[NV];
+#pragma unroll
+        for (int m = 0; m < NV; m++) {
+            v[m] = (int)lane + 64 * m < nf ? sum4((int)lane + 64 * m) : 0.f;
+            a2[m] = v[m] * v[m];
+        }
+        int np = 1;                                  // P / 64
+        while (64 * np < nf) np <<= 1;
+#pragma unroll
+        for (int half = NV / 2; half >= 1; half >>= 1)
+            if (half < np)
+#pragma unroll
+                for (int m = 0; m < half; m++) a2[m] = a2[m] + a2[m + half];
+        float a = a2[0];
 #pragma unroll
         for (int k = 32; k >= 1; k >>= 1) a = a + __shfl_down(a, k, 64);
         const float tot = __shfl(a, 0, 64);
         const float fac = 1.f / sqrtf(tot);
         float* out = desc + ((size_t)f * max_pts + i) * nf;
-        if (lane < (unsigned)nf) out[lane] = v0 * fac;
-        if (nf > 64 && lane + 64 < (unsigned)nf) out[lane + 64] = v1 * fac;
+#pragma unroll
+        for (int m = 0; m < NV; m++)
+            if ((int)lane + 64 * m < nf) out[lane + 64 * m] = v[m] * fac;
         wave_sync();
     }
 }
@@ -2757,7 +2773,7 @@ hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_poin
                            const int* counts, const int* offsets, const int* order, int nframes, float* desc,
                            int* queue, hipStream_t s)
 {
-    if (P.nfeat > 128) return hipErrorInvalidValue;
+    if (P.nfeat > 512) return hipErrorInvalidValue;
     const int grid = 2048;
     hipError_t e = hipMemsetAsync(queue, 0, kDescQueueBytes, s);
     if (e != hipSuccess) return e;
@@ -2765,14 +2781,20 @@ hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_poin
         if (P.extend)
             k_describe_ur<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc, queue);
         else k_describe_ur<false><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc, queue);
+    } else if (P.nfeat > 128) {
+        // windows past 4 x 4 x 8 (desc_wsz 5..7: up to 392 features)
+        if (P.upright)
+            k_describe<true, 512><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, counts, offsets, order, nframes, desc, queue);
+        else
+            k_describe<false, 512><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, counts, offsets, order, nframes, desc, queue);
     } else if (P.upright) {
-        k_describe<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, counts, offsets, order, nframes, desc, queue);
+        k_describe<true, 128><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, counts, offsets, order, nframes, desc, queue);
     } else if (P.wsz == 4 && getenv("SURFHIP_ROT_ATOMIC") == nullptr) {
         if (P.osz == 8)
             k_describe_rot<8><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc, queue);
         else k_describe_rot<4><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc, queue);
     } else {
-        k_describe<false><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, counts, offsets, order, nframes, desc, queue);
+        k_describe<false, 128><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, counts, offsets, order, nframes, desc, queue);
     }
     return hipGetLastError();
 }

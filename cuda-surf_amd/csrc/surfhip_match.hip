@@ -99,7 +99,7 @@ __global__ __launch_bounds__(kMatchThreads) void k_match_part(const float* __res
     }
 }
 
-// Any descriptor length (a multiple of 4, <= 128): runtime trip count.
+// Any descriptor length (a multiple of 4, <= 1024): runtime trip count.
 __global__ __launch_bounds__(kMatchThreads) void k_match_part_any(const float* __restrict__ f1,
                                                                   const float* __restrict__ f2, int n1, int nf,
                                                                   int nscan, int ntile, float* __restrict__ pmx,

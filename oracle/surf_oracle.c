@@ -50,7 +50,11 @@ int or_init_param(or_param* p, int noctaves, float thresh, bool doubled,
 {
     memset(p, 0, sizeof(*p));
     if (noctaves < 1 || noctaves > OR_MAX_OCTAVE) return -1;
-    if (desc_wsz < 1 || 12 % desc_wsz != 0) return -1;
+    /* desc_wsz <= 7: a sample's Gaussian weight is lookup2[(int)(rpos^2 +
+     * cpos^2)] (surfd.cu:1303, 1335, 1999) with |rpos|, |cpos| <
+     * (desc_wsz + 1) / 2, and lookup2 has 40 entries (surfd.cu:23): from
+     * desc_wsz 8 on the reference reads past it */
+    if (desc_wsz < 1 || desc_wsz > 7) return -1;
     p->doubled = doubled;
     p->noctaves = noctaves;
     p->divisor = doubled ? 0.5f : 1.f;
@@ -851,9 +855,10 @@ void or_describe(const or_param* p, const or_geom* g, const int32_t* ii,
      * desc_wsz 4 -- this is the reference's order exactly (its stride loop
      * down to 64, then the warp-synchronous 32 .. 1).  For other window
      * sizes the reference reads its nfeatures-float shared array out of
-     * bounds (tid + 32 >= nf) or, for nf = 72, adds squares twice; here it
-     * is defined as the full sum, which the HIP kernels compute too. */
-    float sq[128];
+     * bounds (tid + 32 >= nf) or, when nf is not a power of two (72, 100,
+     * 200, ...), adds some squares twice; here it is defined as the full sum,
+     * which the HIP kernels compute too. */
+    float sq[512];
     int P = 64;
     while (P < nf) P <<= 1;
     for (int t = 0; t < P; t++) sq[t] = t < nf ? desc[t] * desc[t] : 0.f;

@@ -70,15 +70,19 @@ def test_make_param_matches_oracle(surf, orc):
     for noct in (1, 4, 5, 8):
         for upright in (False, True):
             for extend in (False, True):
-                for wsz in (2, 3, 4, 6):
+                for wsz in (1, 2, 3, 4, 5, 6, 7, 8, 12):
                     for dbl in (False, True):
-                        b = orc.make_param(noct, 4.0, dbl, 9, 2, upright, extend, wsz)
-                        if b.nfeatures > 128:          # the wave-per-keypoint descriptor holds <= 128
+                        nf = wsz * wsz * (8 if extend else 4)
+                        if wsz > 7:                    # the reference reads past lookup2[40]
                             with pytest.raises(surf.SurfError):
                                 surf.make_param(noct, 4.0, dbl, 9, 2, upright, extend, wsz)
+                            with pytest.raises(ValueError):
+                                orc.make_param(noct, 4.0, dbl, 9, 2, upright, extend, wsz)
                             continue
+                        b = orc.make_param(noct, 4.0, dbl, 9, 2, upright, extend, wsz)
                         a = surf.make_param(noct, 4.0, dbl, 9, 2, upright, extend, wsz)
                         assert bytes(a) == bytes(b)
+                        assert a.mag_factor == 12 // wsz and a.nfeatures == nf    # surf.cpp:77-79
 
 
 def test_make_param_rejects_out_of_scope(surf):
@@ -88,6 +92,8 @@ def test_make_param_rejects_out_of_scope(surf):
         surf.make_param(4, 4.0, init_mask_size=5)      # max_scale 3: degenerate lobes
     with pytest.raises(surf.SurfError):
         surf.make_param(0, 4.0)
+    with pytest.raises(surf.SurfError):
+        surf.make_param(4, 4.0, desc_wsz=8)             # weights past lookup2[40] (surfd.cu:23)
 
 
 @pytest.mark.parametrize("init_mask", [6, 9, 12, 15, 18, 20])

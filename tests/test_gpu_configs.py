@@ -128,17 +128,19 @@ def test_candidate_capacity_truncation_is_deterministic(surf, orc):
         assert (np.diff(a["pts"][f]["o"]) >= 0).all()
 
 
-@pytest.mark.parametrize("wsz", [2, 3])
+@pytest.mark.parametrize("wsz,extend", [(2, False), (3, False), (5, False), (5, True), (6, True), (7, True)])
 @pytest.mark.parametrize("upright", [True, False])
-def test_descriptor_window_sizes(surf, orc, wsz, upright):
-    """desc_wsz 2 and 3 (mag_factor 6 / 4, 16- and 36-D) on the generic
-    k_describe (surfd.cu:1566-1615, 2391-2444 with wsz != 4)."""
+def test_descriptor_window_sizes(surf, orc, wsz, extend, upright):
+    """desc_wsz other than 4 on the generic k_describe (surfd.cu:1566-1615,
+    2391-2444 with wsz != 4): 16-, 36-, 100-, 200-, 288- and 392-D (mag_factor
+    12 / wsz = 6, 4, 2, 2, 2, 1); windows past 4 x 4 x 8 use the 512-feature
+    instance."""
     w, h = 640, 480
     frames = surf.synth_frames(2, w, h, first=40)
-    param = surf.make_param(4, 4.0, upright=upright, desc_wsz=wsz)
-    assert param.nfeatures == wsz * wsz * 4
+    param = surf.make_param(4, 4.0, upright=upright, extend=extend, desc_wsz=wsz)
+    assert param.nfeatures == wsz * wsz * (8 if extend else 4)
     res = gpu_run(surf, param, frames, w, h)
-    op = orc.make_param(4, 4.0, upright=upright, desc_wsz=wsz)
+    op = orc.make_param(4, 4.0, upright=upright, extend=extend, desc_wsz=wsz)
     for f in range(2):
         o_pts, o_desc, _ = orc.detect(op, frames[f], w, h)
         assert len(o_pts) > 100

@@ -404,7 +404,8 @@ def test_match_golden_left_right(surf, orc, tag, flags):
 
 @pytest.mark.parametrize("n1,n2,nf,flags", [(1, 0, 64, 0), (7, 31, 64, 0), (7, 31, 64, 1), (300, 545, 64, 0),
                                              (300, 545, 64, 1), (1000, 4096, 64, 0), (3000, 3000, 64, 1),
-                                             (257, 700, 128, 0), (129, 333, 36, 1), (64, 64, 16, 0)])
+                                             (257, 700, 128, 0), (129, 333, 36, 1), (64, 64, 16, 0),
+                                             (200, 333, 200, 0), (70, 90, 392, 1)])
 def test_match_random_vs_oracle(surf, orc, n1, n2, nf, flags):
     rng = np.random.default_rng(n1 + 7 * n2 + nf + flags)
     f1 = rng.standard_normal((n1, nf)).astype(np.float32)

@@ -678,11 +678,13 @@ def test_oracle_sanitizer_build():
     assert out.returncode == 0 and "asan ok" in out.stdout, out.stdout[-2000:] + out.stderr[-2000:]
 
 
-@pytest.mark.parametrize("wsz,extend", [(2, False), (3, False), (3, True), (4, False), (4, True)])
+@pytest.mark.parametrize("wsz,extend", [(2, False), (3, False), (3, True), (4, False), (4, True), (5, True),
+                                        (6, False), (7, True)])
 def test_descriptors_unit_norm_every_window(orc, wsz, extend):
-    """normalize sums every square for any nfeatures (16, 36, 72, 64, 128):
-    unit L2 norm (the reference's tree reads out of bounds below 64 and
-    double-adds at 72; DESIGN.md, fixed semantics)."""
+    """normalize sums every square for any nfeatures (16, 36, 72, 64, 128,
+    200, 144, 392): unit L2 norm (the reference's tree reads out of bounds
+    below 64 and double-adds where nfeatures is not a power of two; DESIGN.md,
+    fixed semantics)."""
     img = np.load(os.path.join(GOLDEN, "images.npz"))["left_640x480"]
     p = orc.make_param(4, 4.0, upright=False, extend=extend, desc_wsz=wsz)
     pts, d, _ = orc.detect(p, img, 640, 480)

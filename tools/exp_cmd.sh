@@ -1,7 +1,2 @@
-set -u
-cd /tmp && export TMPDIR=/tmp
-cd "${GRAFT_REPO_ROOT:-/root/repo}"
-mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/final_pytest.log 2>&1 || { tail -30 gpurun_out/final_pytest.log; exit 1; }
-tail -1 gpurun_out/final_pytest.log
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('SMOKE_OK')" 2>&1 | tail -1
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "window_sizes or match_random or golden or surfor" > gpurun_out/wsz_pytest.log 2>&1; tail -3 gpurun_out/wsz_pytest.log
+bash tools/pd_ab.sh "default prio1 prio2 prio0" "93"
