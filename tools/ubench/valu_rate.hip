@@ -22,6 +22,12 @@ __global__ __launch_bounds__(256) void k(float* out, int iters)
             if (KIND == 2) asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(a[i]) : "v"(c));
             if (KIND == 3) asm volatile("v_add_u32 %0, %0, %0" : "+v"(u[i]));
             if (KIND == 4) asm volatile("v_fma_f32 %0, %0, %0, %0" : "+v"(b[i]));
+            if (KIND == 5) asm volatile("v_dot4_u32_u8 %0, %0, %0, %0" : "+v"(u[i]));
+            if (KIND == 6) asm volatile("v_lshl_add_u32 %0, %0, 1, %0" : "+v"(u[i]));
+            if (KIND == 7) asm volatile("v_cvt_f32_u32 %0, %0" : "+v"(b[i]));
+            if (KIND == 8) asm volatile("s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(u[i]));
+            if (KIND == 9) asm volatile("v_add3_u32 %0, %0, %0, %0" : "+v"(u[i]));
+            if (KIND == 10) asm volatile("v_sub_f32 %0, %0, %0" : "+v"(b[i]));
         }
     }
     float s = 0;
@@ -36,9 +42,10 @@ int main()
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    const char* names[] = {"v_add_f32", "v_pk_add_f32", "v_pk_fma_f32", "v_add_u32", "v_fma_f32"};
+    const char* names[] = {"v_add_f32", "v_pk_add_f32", "v_pk_fma_f32", "v_add_u32", "v_fma_f32", "v_dot4_u32_u8",
+                           "v_lshl_add_u32", "v_cvt_f32_u32", "nop1+v_add_dpp", "v_add3_u32", "v_sub_f32"};
     const int iters = 20000;
-    for (int kind = 0; kind < 5; kind++) {
+    for (int kind = 0; kind < 11; kind++) {
         for (int wps : {1, 2, 4}) {
             // 256 CUs x 4 SIMDs x wps waves, 4 waves per workgroup
             const int blocks = 256 * wps;
@@ -49,6 +56,12 @@ int main()
                     case 2: k<2><<<blocks, 256>>>(out, iters); break;
                     case 3: k<3><<<blocks, 256>>>(out, iters); break;
                     case 4: k<4><<<blocks, 256>>>(out, iters); break;
+                    case 5: k<5><<<blocks, 256>>>(out, iters); break;
+                    case 6: k<6><<<blocks, 256>>>(out, iters); break;
+                    case 7: k<7><<<blocks, 256>>>(out, iters); break;
+                    case 8: k<8><<<blocks, 256>>>(out, iters); break;
+                    case 9: k<9><<<blocks, 256>>>(out, iters); break;
+                    case 10: k<10><<<blocks, 256>>>(out, iters); break;
                 }
             };
             launch();
