@@ -811,6 +811,15 @@ struct OctView {
         return base + r * (h ? hr + (p1 ? dhr : 0) : sp) + c * (h ? hc + (p1 ? dhc : 0) : 1);
     }
     __device__ __forceinline__ float operator()(int s, int r, int c) const { return F[off(s, r, c)]; }
+    // (s, r, c) and (s, r, c + 1) of a plane that is not a halfImage view:
+    // one 8-byte load (4-byte aligned)
+    __device__ __forceinline__ void pair_full(int s, int r, int c, float& a, float& b) const
+    {
+        typedef float f2a4 __attribute__((ext_vector_type(2), aligned(4)));
+        const f2a4 v = *reinterpret_cast<const f2a4*>(F + cur + s * osize + r * sp + c);
+        a = v.x;
+        b = v.y;
+    }
     // (s, r, c) and (s, r, c + 1)
     __device__ __forceinline__ void pair(int s, int r, int c, float& a, float& b) const
     {
@@ -997,7 +1006,9 @@ __device__ __forceinline__ int wave_append(bool ok, int* counter)
 // One workgroup = 4 waves x (64 block columns x kScanRows/4 block rows) of
 // one (frame, octave, level), a wave's rows in passes of 4 whose loads are
 // issued one pass ahead; XCD x takes frames x, x + 8, ...
-template <bool CUBE>
+// HK: plane k of this item is a halfImage view (octave > 0, level 1): its
+// column pairs are two loads; every other pair is one 8-byte load
+template <bool CUBE, bool HK>
 __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, const FrameParams& P,
                                               const OctaveParams* __restrict__ oct, const LaunchPlan& plan,
                                               uint32_t* __restrict__ scan_key, uint32_t* __restrict__ scan_src,
@@ -1035,10 +1046,15 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
             const int y = ybase + 4 * (it * NU + u), i = mb + y * 2;
             inn[u] = x < q.nms_gx && y < q.nms_gy && i < q.sh - mb && j < q.sw - mb;
             const int ii = inn[u] ? i : mb, jj = inn[u] ? j : mb;
-            V.pair(k, ii, jj, vv[u][0], vv[u][1]);
-            V.pair(k, ii + 1, jj, vv[u][2], vv[u][3]);
-            V.pair(k + 1, ii, jj, vv[u][4], vv[u][5]);
-            V.pair(k + 1, ii + 1, jj, vv[u][6], vv[u][7]);
+            if constexpr (HK) {
+                V.pair(k, ii, jj, vv[u][0], vv[u][1]);
+                V.pair(k, ii + 1, jj, vv[u][2], vv[u][3]);
+            } else {
+                V.pair_full(k, ii, jj, vv[u][0], vv[u][1]);
+                V.pair_full(k, ii + 1, jj, vv[u][2], vv[u][3]);
+            }
+            V.pair_full(k + 1, ii, jj, vv[u][4], vv[u][5]);
+            V.pair_full(k + 1, ii + 1, jj, vv[u][6], vv[u][7]);
         }
     };
     load(0, v[0], in[0]);
@@ -1200,9 +1216,15 @@ __global__ __launch_bounds__(256) void k_nms_scan(const float* __restrict__ resp
     int f, gb;
     if (!xcd_frame_block(plan.nms_start[kMaxOct], nframes, f, gb)) return;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    nms_scan_item<CUBE>(resp, P, oct, plan, scan_key, scan_src, scan_cube, item_count, plan.nms_start[kMaxOct], f, gb, wv,
-                  sbest[wv],
-                  sinfo[wv], sblk[wv]);
+    // plane k (= 2 z + 1) is a halfImage view for octaves > 0 at level z = 0
+    const int o = octave_of(plan.nms_start, P.noct, gb);
+    const int z = (gb - plan.nms_start[o]) / (plan.nms_nbx[o] * plan.nms_nby[o]);
+    if (o > 0 && z == 0)
+        nms_scan_item<CUBE, true>(resp, P, oct, plan, scan_key, scan_src, scan_cube, item_count,
+                                  plan.nms_start[kMaxOct], f, gb, wv, sbest[wv], sinfo[wv], sblk[wv]);
+    else
+        nms_scan_item<CUBE, false>(resp, P, oct, plan, scan_key, scan_src, scan_cube, item_count,
+                                   plan.nms_start[kMaxOct], f, gb, wv, sbest[wv], sinfo[wv], sblk[wv]);
 }
 
 // Exclusive prefix of n ints (n up to ~2M): each workgroup scans 2048
