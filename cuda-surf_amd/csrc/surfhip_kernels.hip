@@ -1676,6 +1676,19 @@ __device__ __forceinline__ float sincos_poly(float x, int want_cos)
     }
 }
 
+// x / y as the IEEE quotient, from r = 1 / y (IEEE, once per keypoint): q0 =
+// x r, q = q0 + (x - q0 y) r with the remainder exact (fma).  This is the
+// correctly rounded x / y whenever the quotient is a normal number (Markstein;
+// 0 mismatches in 8.5e8 trials incl. all-ones significands of y); for |x / y|
+// below 2^-100 it may differ in the last bits of a value that only ever enters
+// rpos + wofs and rpos^2 + cpos^2, where it vanishes.  3 full-rate
+// instructions instead of the ~10 of the IEEE division sequence.
+__device__ __forceinline__ float div_by(float x, float y, float r)
+{
+    const float q0 = x * r;
+    return __builtin_fmaf(__builtin_fmaf(-q0, y, x), r, q0);
+}
+
 // placeInIndex (surfd.cu:1199-1271) into an LDS descriptor.
 __device__ __forceinline__ void place(float* d, int wsz, int osz, float mag1, int ori1, float mag2, int ori2,
                                       float rx, float cx)
@@ -1929,6 +1942,7 @@ __global__ __launch_bounds__(256) void k_describe(const int32_t* __restrict__ ii
         const int step = max(f2i_rn(scale * 0.5f), 1);
         const int ix = f2i_rn(at.x), iy = f2i_rn(at.y);
         const float spacing = scale * (float)P.mag;
+        const float rspacing = 1.f / spacing;
         const int hs = f2i_rz(scale);
         const int rlim = P.iH - 1 - hs, clim = P.W - hs;   // whps[1].y-1-s, whps[1].x-1-s
         if constexpr (UPRIGHT) {
@@ -1938,8 +1952,8 @@ __global__ __launch_bounds__(256) void k_describe(const int32_t* __restrict__ ii
             const int nsamp = side * side;
             for (int t = lane; t < nsamp; t += 64) {
                 const int si = t / side - iradius, sj = t % side - iradius;
-                const float rpos = ((float)(step * si) - dy0) / spacing;
-                const float cpos = ((float)(step * sj) - dx0) / spacing;
+                const float rpos = div_by((float)(step * si) - dy0, spacing, rspacing);
+                const float cpos = div_by((float)(step * sj) - dx0, spacing, rspacing);
                 const float rx = rpos + wofs, cx = cpos + wofs;
                 if (!(rx > -1.f && rx < fw && cx > -1.f && cx < fw)) continue;
                 const int r = iy + si * step, c = ix + sj * step;
@@ -1966,8 +1980,8 @@ __global__ __launch_bounds__(256) void k_describe(const int32_t* __restrict__ ii
             for (int t = lane; t < nsamp; t += 64) {
                 const int si = t / side - iradius, sj = t % side - iradius;
                 const float fi = (float)si, fj = (float)sj;
-                const float rpos = ((fstep * ((cose * fi) + (sine * fj))) - fracr) / spacing;
-                const float cpos = ((fstep * (((-sine) * fi) + (cose * fj))) - fracc) / spacing;
+                const float rpos = div_by((fstep * ((cose * fi) + (sine * fj))) - fracr, spacing, rspacing);
+                const float cpos = div_by((fstep * (((-sine) * fi) + (cose * fj))) - fracc, spacing, rspacing);
                 const float rx = rpos + wofs, cx = cpos + wofs;
                 if (!(rx > -1.f && rx < fw && cx > -1.f && cx < fw)) continue;
                 const int r = iy + si * step, c = ix + sj * step;
@@ -2092,6 +2106,7 @@ __global__ __launch_bounds__(256) void k_describe_rot(const int32_t* __restrict_
         const float fracr = (cose * fracy) + (sine * fracx);
         const int iradius = f2i_rn((((1.4f * spacing) * (float)(WSZ + 1)) * 0.5f) / (float)step);
         const float fstep = (float)step;
+        const float rspacing = 1.f / spacing;
         // grid box of this lane's cell: inverse rotation of its corners
         int i0 = 1, i1 = 0, j0 = 0, j1 = 0;
         if (owner) {
@@ -2156,11 +2171,12 @@ __global__ __launch_bounds__(256) void k_describe_rot(const int32_t* __restrict_
             }
             const int cj = sj++;
             const float fi = (float)si, fj = (float)cj;
-            // IEEE division as the reference: rpos^2 + cpos^2 indexes the
+            // the IEEE quotient as the reference: rpos^2 + cpos^2 indexes the
             // Gaussian LUT, so one ulp can move a sample to the next weight
-            // (x * (1 / spacing) broke config #5 parity at 1.3e-3 L2)
-            const float rpos = ((fstep * ((cose * fi) + (sine * fj))) - fracr) / spacing;
-            const float cpos = ((fstep * (((-sine) * fi) + (cose * fj))) - fracc) / spacing;
+            // (x * (1 / spacing) alone broke config #5 parity at 1.3e-3 L2);
+            // div_by is exact where it matters
+            const float rpos = div_by((fstep * ((cose * fi) + (sine * fj))) - fracr, spacing, rspacing);
+            const float cpos = div_by((fstep * (((-sine) * fi) + (cose * fj))) - fracc, spacing, rspacing);
             const float rx = rpos + wofs, cx = cpos + wofs;
             if (!(rx > -1.f && rx < fw && cx > -1.f && cx < fw)) continue;
             const int ri = f2i_rz(rx >= 0.f ? rx : rx - 1.f);
@@ -2169,8 +2185,13 @@ __global__ __launch_bounds__(256) void k_describe_rot(const int32_t* __restrict_
             const int r = iy + si * step, c = ix + cj * step;
             if (!(r >= 1 + hs && r < rlim && c >= 1 + hs && c < clim)) continue;
             const float weight = c_tab.lut2[f2i_rz(rpos * rpos + cpos * cpos)];
+#ifdef SURF_DIAG_ROT_NOLOAD
+            const float dxx = (weight * (float)(r * 7 - c)) * INV255;
+            const float dyy = (weight * (float)(c * 3 + r)) * INV255;
+#else
             const float dxx = (weight * (float)wavelet2(I, ip, c, r, hs)) * INV255;
             const float dyy = (weight * (float)wavelet1(I, ip, c, r, hs)) * INV255;
+#endif
             const float dx = (cose * dxx) + (sine * dyy);
             const float dy = (sine * dxx) - (cose * dyy);
             const float rfrac = rx - (float)ri, cfrac = cx - (float)ci;
