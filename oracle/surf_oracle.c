@@ -1037,3 +1037,42 @@ void or_match(or_point* pts1, const or_point* pts2, const float* f1, const float
         q->ambiguity = sc / (mx + 1e-6f);
     }
 }
+
+/* Checker for the HIP kernels' descriptor-position quotient (div_by in
+ * surfhip_kernels.hip: q0 = x r, q = fma(fma(-q0, y, x), r, q0) with r =
+ * 1 / y): counts, over n pseudo-random (x, y) in the ranges the descriptor
+ * kernels see (y = 3 * (1.65 * scale), scale in [1, 80); |x| < 400, or any
+ * normal |x| >= 2^-100 against y of every exponent 2^1 .. 2^8 with random or
+ * all-ones significands), the trials where q differs from the IEEE x / y.
+ * Test infrastructure only. */
+long or_div_by_mismatches(long n, uint64_t seed)
+{
+    uint64_t s = seed | 1u;
+    long bad = 0;
+    for (long i = 0; i < n; i++) {
+        s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+        const uint64_t a = s;
+        s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+        const uint64_t b = s;
+        float x, y;
+        if (i & 1) {
+            const float scale = 1.f + (float)(a % 1000000u) * 7.9e-5f;
+            y = 3.0f * (1.65f * scale);
+            x = ((float)((int64_t)(b % 8000001u) - 4000000)) * 1e-4f;
+        } else {
+            const uint32_t m = (a & 1u) ? 0x7FFFFFu - (uint32_t)((a >> 1) % 2048u) : (uint32_t)((a >> 1) & 0x7FFFFFu);
+            const uint32_t e = 128u + (uint32_t)((a >> 40) % 8u);
+            const uint32_t yu = (e << 23) | m;
+            const uint32_t xu = (0x0D800000u + (uint32_t)(b % (0x43800000u - 0x0D800000u))) | ((uint32_t)(b >> 63) << 31);
+            memcpy(&y, &yu, 4);
+            memcpy(&x, &xu, 4);
+        }
+        volatile float yy = y;
+        const float r = 1.0f / yy;
+        const float q0 = x * r;
+        const float q = fmaf(fmaf(-q0, y, x), r, q0);
+        const float ref = x / yy;
+        if (q != ref) bad++;
+    }
+    return bad;
+}

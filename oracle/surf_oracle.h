@@ -158,6 +158,8 @@ void or_match(or_point* pts1, const or_point* pts2, const float* f1, const float
               int n1, int n2, int nf, int full_tail);
 
 /* Deterministic sine/cosine used in place of __sinf/__cosf. */
+/* test infrastructure: mismatches of the kernels' x * r + remainder quotient */
+long or_div_by_mismatches(long n, uint64_t seed);
 float or_sinf(float x);
 float or_cosf(float x);
 /* dFastAtan2 (surfd.cu:114-126). */

@@ -691,3 +691,16 @@ def test_descriptors_unit_norm_every_window(orc, wsz, extend):
     assert len(pts) > 100 and d.shape[1] == wsz * wsz * (8 if extend else 4)
     n = np.sqrt((d.astype(np.float64) ** 2).sum(1))
     assert np.abs(n - 1).max() < 1e-5
+
+
+def test_descriptor_quotient_matches_ieee_division(orc):
+    """The descriptor kernels compute rpos / cpos as x * r + fma remainder
+    correction (r = 1 / spacing once per keypoint, surfhip_kernels.hip
+    div_by) instead of the reference's per-sample division (surfd.cu:1290-1292,
+    2420-2430): the quotient must be the IEEE one, since rpos^2 + cpos^2
+    indexes the Gaussian LUT."""
+    import ctypes as C
+    fn = orc._L.or_div_by_mismatches
+    fn.restype = C.c_long
+    fn.argtypes = [C.c_long, C.c_uint64]
+    assert fn(20_000_000, 12345) == 0
