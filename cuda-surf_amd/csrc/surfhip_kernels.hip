@@ -2320,6 +2320,19 @@ __device__ __forceinline__ void haar_bins(int32_t wav1, int32_t wav2, float weig
 
 template <int R> struct IntC { static constexpr int value = R; };
 
+// value of lane - 2 / lane + 2 across the whole wave (DPP wave_shr:1 /
+// wave_shl:1 twice; lanes shifted in from outside the wave get 0)
+__device__ __forceinline__ uint32_t wave_from_lo2(uint32_t v)
+{
+    const int a = __builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, a, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wave_from_hi2(uint32_t v)
+{
+    const int a = __builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, a, 0x130, 0xf, 0xf, false);
+}
+
 template <bool EXT>
 __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__ ii, FrameParams P,
                                                      const surfhip_point* __restrict__ pts, int max_pts,
@@ -2526,12 +2539,14 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
             auto rows = [&](auto AC) {
                 constexpr bool A = decltype(AC)::value;
                 // T = rows r, r+1 x cols c-s, c, c+1, c+s+1
+                // columns c -+ hs from lanes j -+ 2: two DPP wave shifts each
+                // (VALU) instead of an LDS permute
                 auto proc = [&](const Raw& q, uint32_t (&T)[8]) {
                     T[1] = q.lo.x; T[2] = q.lo.y; T[5] = q.hi.x; T[6] = q.hi.y;
-                    const uint32_t l0 = (uint32_t)__shfl((int)(A ? q.lo.x : q.lo.y), lane - 2, 64);
-                    const uint32_t r0 = (uint32_t)__shfl((int)(A ? q.lo.y : q.lo.x), lane + 2, 64);
-                    const uint32_t l1 = (uint32_t)__shfl((int)(A ? q.hi.x : q.hi.y), lane - 2, 64);
-                    const uint32_t r1 = (uint32_t)__shfl((int)(A ? q.hi.y : q.hi.x), lane + 2, 64);
+                    const uint32_t l0 = wave_from_lo2(A ? q.lo.x : q.lo.y);
+                    const uint32_t r0 = wave_from_hi2(A ? q.lo.y : q.lo.x);
+                    const uint32_t l1 = wave_from_lo2(A ? q.hi.x : q.hi.y);
+                    const uint32_t r1 = wave_from_hi2(A ? q.hi.y : q.hi.x);
                     T[0] = eL ? q.elo : l0;
                     T[3] = eR ? q.elo : r0;
                     T[4] = eL ? q.ehi : l1;
