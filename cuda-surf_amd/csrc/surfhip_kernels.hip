@@ -1027,6 +1027,7 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
     const int x = (lb % nbx) * 64 + (int)lane_id();
     const int ybase = (lb / nbx) * kScanRows + wv;     // this wave: rows ybase + 4 u, u < 4 NIT
     const OctView V = make_view(resp + (size_t)f * P.resp_stride, q, o);
+    const rsrc_t RF = make_rsrc(resp + (size_t)f * P.resp_stride, (long long)P.resp_stride * 4);
     const int k = 2 * z + 1, mb = q.mb[z];
     const int j = mb + x * 2;
     const int bx0 = (lb % nbx) * 64;
@@ -1078,6 +1079,25 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
             for (int t = 1; t < 8; t++)
                 if (vc[u][t] > best) { best = vc[u][t]; cas = t; }
             cnd[u] = ic[u] && !(best < P.thresh * 0.8f || (k + 1 == P.max_scale - 1 && cas > 3));
+#ifdef SURF_DIAG_NMS_NOCAND
+            if (best != -1.2345f) cnd[u] = false;
+#endif
+#ifndef SURF_NMS_NOPRE
+            // 4 of the 19 neighbours, (s / si, r / rp, cn), are the adjacent
+            // block column of lane -+ 1 (the same block row): a candidate below
+            // any of them cannot survive, so it is dropped before the gathers
+            // (same result; a lane whose neighbour block lies outside the grid
+            // or the wave keeps its candidate for the full test)
+            const float ninf = -__builtin_inff();
+            const float lmax = ic[u] ? fmaxf(fmaxf(vc[u][0], vc[u][2]), fmaxf(vc[u][4], vc[u][6])) : ninf;
+            const float rmax = ic[u] ? fmaxf(fmaxf(vc[u][1], vc[u][3]), fmaxf(vc[u][5], vc[u][7])) : ninf;
+            // lane - 1's right column (wave_shr:1) / lane + 1's left column (wave_shl:1)
+            const float fromL = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(ninf), __float_as_int(rmax),
+                                                                           0x138, 0xf, 0xf, false));
+            const float fromR = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(ninf), __float_as_int(lmax),
+                                                                           0x130, 0xf, 0xf, false));
+            cnd[u] = cnd[u] && !(best < ((cas & 1) ? fromR : fromL));
+#endif
             bst[u] = best;
             cs[u] = cas;
         }
@@ -1121,21 +1141,49 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
                 ds = (cas >> 2) ? 1 : -1; dr = ((cas >> 1) & 1) ? 1 : -1; dc = (cas & 1) ? 1 : -1;
                 const int so = s + ds, si = s - ds;
                 const int rn = r + dr, rp = r - dr, cn = c + dc;
-                // the 19 neighbours outside the block, ties survive (surfd.cu:757-792);
-                // all loads issued before any compare
-                const float nbv[19] = {V(so, rp, c - 1), V(so, rp, c), V(so, rp, c + 1),
-                                       V(so, r, c - 1),  V(so, r, c),  V(so, r, c + 1),
-                                       V(so, rn, c - 1), V(so, rn, c), V(so, rn, c + 1),
-                                       V(s, rn, c - 1),  V(s, rn, c),  V(s, rn, c + 1),
-                                       V(s, r, cn),      V(s, rp, cn),
-                                       V(si, rn, c - 1), V(si, rn, c), V(si, rn, c + 1),
-                                       V(si, rp, cn),    V(si, r, cn)};
+                // the 19 neighbours outside the block, ties survive (surfd.cu:757-792),
+                // in six rounds, each only for the candidates the previous
+                // ones left: plane s's row rn, its column cn, plane si, then
+                // plane so's rows r, rp, rn.  Gathers for every candidate cost
+                // half the scan (0.87 ms with all 19 up front, 0.42 without
+                // any); in rounds with 12-byte row loads it takes 0.69.
+#ifdef SURF_DIAG_NMS_NONB
+#define NBV(pl, rr, cc) (best + (float)((pl) + (rr) + (cc)))
+#else
+#define NBV(pl, rr, cc) V(pl, rr, cc)
+#endif
                 ok = true;
-#pragma unroll
-                for (int t = 0; t < 19; t++) {
-                    nb[t] = nbv[t];
-                    ok = ok && !(best < nbv[t]);
-                }
+                // one round of the test: its loads, then its compares (nb keeps
+                // the values for the fit record)
+                auto test = [&](int at, float v) {
+                    nb[at] = v;
+                    ok = ok & !(best < v);          // '&': no branch between the loads and a compare
+                };
+                // (pl, rr, c - 1 .. c + 1): one 12-byte load where plane pl is
+                // not a halfImage view
+                auto row3 = [&](int at, int pl, int rr) {
+                    float a0, a1, a2;
+#ifdef SURF_DIAG_NMS_NONB
+                    a0 = NBV(pl, rr, c - 1); a1 = NBV(pl, rr, c); a2 = NBV(pl, rr, c + 1);
+#else
+                    if (HK && pl < 2) {
+                        a0 = V(pl, rr, c - 1); a1 = V(pl, rr, c); a2 = V(pl, rr, c + 1);
+                    } else {
+                        typedef uint32_t v3u32 __attribute__((ext_vector_type(3)));
+                        const v3u32 t3 = __builtin_amdgcn_raw_buffer_load_b96(
+                            RF, (V.cur + pl * V.osize + rr * V.sp + c - 1) * 4, 0, 0);
+                        a0 = __uint_as_float(t3.x); a1 = __uint_as_float(t3.y); a2 = __uint_as_float(t3.z);
+                    }
+#endif
+                    test(at, a0); test(at + 1, a1); test(at + 2, a2);
+                };
+                row3(9, s, rn);
+                if (ok) { test(12, NBV(s, r, cn)); test(13, NBV(s, rp, cn)); }
+                if (ok) { row3(14, si, rn); test(17, NBV(si, rp, cn)); test(18, NBV(si, r, cn)); }
+                if (ok) row3(3, so, r);
+                if (ok) row3(0, so, rp);
+                if (ok) row3(6, so, rn);
+#undef NBV
             }
             const unsigned long long mo = __ballot(ok);
             if (ok) {
