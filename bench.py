@@ -341,7 +341,8 @@ def run_rank(args):
             if rank == 0:
                 uid[:] = torch.frombuffer(bytearray(surf.comm_unique_id()), dtype=torch.uint8)
             dist.broadcast(uid, 0)
-            comm = surf.Comm(world, rank, bytes(uid.numpy().tobytes()))
+            with _StdoutToStderr():
+                comm = surf.Comm(world, rank, bytes(uid.numpy().tobytes()))
 
     nstep = 0                                          # buffer i & 1 across warmup and timed steps
     timing = [False]
@@ -487,7 +488,8 @@ def run_rank(args):
     # (libsurfcomm) of the real slab, both modes, after the timed region
     probe = None
     if world == 1 and not args.hessian_only and not args.no_exchange_probe:
-        probe = exchange_probe(surf, torch, det, dev, stream, d_pts, d_desc, d_cnt, B, nf)
+        with _StdoutToStderr():
+            probe = exchange_probe(surf, torch, det, dev, stream, d_pts, d_desc, d_cnt, B, nf)
 
     frames_total = world * B * args.steps
     value = frames_total / elapsed
@@ -543,6 +545,24 @@ def run_rank(args):
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+class _StdoutToStderr:
+    """RCCL prints its version banner on fd 1 when a communicator comes up;
+    the bench's stdout carries only the JSON line, so fd 1 points at fd 2
+    while libsurfcomm runs."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
 
 
 def exchange_probe(surf, torch, det, dev, stream, d_pts, d_desc, d_cnt, B, nf, reps=5):

@@ -197,7 +197,9 @@ def test_bench_single_gpu_exchange_probe():
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--batch", "8", "--steps", "3",
                         "--warmup", "1", "--no-cpu"], capture_output=True, text=True, timeout=240, cwd=REPO)
     assert r.returncode == 0, r.stderr[-3000:]
-    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout      # RCCL's banner goes to stderr
+    d = json.loads(lines[0])
     ex = d["exchange"]
     assert "error" not in ex, ex
     assert ex["full"]["bytes_equal"] and ex["points"]["bytes_equal"]
