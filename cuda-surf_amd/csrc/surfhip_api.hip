@@ -599,19 +599,15 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
         // the u8 Hessian kernels (octaves 0, 1) need no integral image: they run
         // on s beside the integral and the integral-image Hessian kernels
         // (octaves >= 2) on the side stream; s waits for both
-        static const bool w_side = getenv("SURFHIP_W_SIDE") && atoi(getenv("SURFHIP_W_SIDE")) != 0;
         HIPCHK(source_frames(d, frames, pitch, stride, nframes, s));
         HIPCHK(hipEventRecord(d->fork, s));
         HIPCHK(hipStreamWaitEvent(d->side, d->fork, 0));
-        if (w_side)
-            HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
-                                  d->plan, d->side, 4));
         HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, d->side));
         HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
                               d->plan, d->side, 2));
         HIPCHK(hipEventRecord(d->join, d->side));
         HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
-                              d->plan, s, w_side ? 1 | 8 : 1));
+                              d->plan, s, 1));
         HIPCHK(hipStreamWaitEvent(s, d->join, 0));
     }
     HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->scan_key, d->scan_src, d->scan_cube,

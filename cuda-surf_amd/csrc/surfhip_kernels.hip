@@ -715,10 +715,8 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
     const int nf8 = (nframes + 7) & ~7;
     // parts: 1 = the kernels that read the u8 frames, 2 = those that read the
     // integral image (the two may run on different streams)
-    // 4 = k_hess_w alone, 8 = the u8 kernels without k_hess_w
     const bool u8p = (parts & 1) != 0, iip = (parts & 2) != 0;
-    const bool wp = (parts & 4) != 0 || (u8p && (parts & 8) == 0);
-    if ((u8p || wp) && !frames && (plan.q0 || plan.q1 || plan.hw_n > 0)) return hipErrorInvalidValue;
+    if (u8p && !frames && (plan.q0 || plan.q1 || plan.hw_n > 0)) return hipErrorInvalidValue;
     if (u8p) {
         const int nb0 = 8 * (((nf8 / 8) * plan.q0_strips + q0::WAVES - 1) / q0::WAVES);
         const int nb1 = 8 * (((nf8 / 8) * plan.q1_strips + q1::WAVES - 1) / q1::WAVES);
@@ -741,8 +739,6 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
                 k_hess_q1<2><<<dim3(nb1), q1::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[1],
                                                                plan.q1_strips, nframes);
         }
-    }
-    if (wp) {
         if (plan.hw_n > 0) {
             const dim3 g(nf8 * plan.hw_nstrips);
             const OctaveParams& q3 = h_oct[plan.hw_n >= 3 ? 3 : 2];
