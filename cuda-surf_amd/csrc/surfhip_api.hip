@@ -441,6 +441,11 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     d->stream = (hipStream_t)stream;
     hipError_t e = hipGetDevice(&d->dev);
     rc = (e == hipSuccess) ? derive(d) : SURFHIP_ERR_HIP;
+    // the NMS survivor records pack the sample row / column into 14 bits and
+    // the block row of the canonical key into 13 (k_nms_scan): octave 0 is
+    // the largest octave, so its extent bounds them all
+    if (rc == SURFHIP_OK && (d->oct[0].sh >= 16384 || d->oct[0].sw >= 16384 || d->oct[0].nms_gy >= 8192))
+        rc = SURFHIP_ERR_UNSUPPORTED;
     if (rc != SURFHIP_OK) {
         if (e != hipSuccess) g_last_hip = e;
         delete d;
@@ -570,6 +575,8 @@ int surfhip_run_integral(surfhip_detector* d, const uint8_t* frames, int nframes
 int surfhip_run_hessian(surfhip_detector* d, int nframes)
 {
     if (!d || nframes < 1 || nframes > d->max_batch) return SURFHIP_ERR_INVALID;
+    // the u8 Hessian kernels read the frames of the last run_integral
+    if (!d->last_frames && plan_reads_frames(d->plan)) return SURFHIP_ERR_INVALID;
     HIPCHK(launch_hessian(d->last_frames, d->last_pitch, d->last_fstride, d->ii, d->resp, nframes, d->P, d->d_oct,
                           d->oct, d->plan, d->stream));
     return SURFHIP_OK;

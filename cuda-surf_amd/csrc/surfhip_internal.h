@@ -96,6 +96,8 @@ struct LaunchPlan {
     int hw_n;                       // octaves 1 .. hw_n on k_hess_w (u8, shared strip integral); 0: off
     int hw_nstrips, hw_nblk;        // its strips per frame and blocks of 4 integral rows
 };
+// the plan has kernels that read the u8 frames (not only the integral image)
+inline bool plan_reads_frames(const LaunchPlan& p) { return p.q0 || p.q1 || p.hw_n > 0; }
 // max_batch <= kGatherBatch (or SURFHIP_HESS_GATHER=1; =0 disables) puts every
 // octave on the one-thread-per-response gather kernel: the streaming kernels
 // walk whole strips, one wave each, too few waves to fill the chip for a few

@@ -185,7 +185,10 @@ __device__ __forceinline__ void load_px(const uint8_t* row, int x0, int W, uint3
         for (int k = 0; k < 8; k++) px[k] = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
     } else if constexpr (CPT == 32) {
         const uint4 a = *reinterpret_cast<const uint4*>(row + x0);
-        const uint4 b = *reinterpret_cast<const uint4*>(row + x0 + 16);
+        // the second half only where it holds frame columns: the caller's
+        // pitch is a multiple of 16, not of 32, so x0 + 16 >= W may lie past
+        // the row (and past the buffer on the last row)
+        const uint4 b = (x0 + 16 < W) ? *reinterpret_cast<const uint4*>(row + x0 + 16) : make_uint4(0u, 0u, 0u, 0u);
         const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
         for (int k = 0; k < 32; k++) px[k] = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;

@@ -106,7 +106,9 @@ int  surfhip_event_elapsed(float* ms, void* start, void* stop);
 typedef struct surfhip_detector surfhip_detector;
 
 /* Surfor::init + allocMemory (surf.cpp:60-91, 374-415).  `param` must come
- * from surfhip_make_param.  cand_cap = per-frame candidate capacity before
+ * from surfhip_make_param.  Frames up to 8,191 columns (after doubling) and
+ * octave-0 sample grids below 16,384 x 16,384 (NMS record fields);
+ * SURFHIP_ERR_UNSUPPORTED otherwise.  cand_cap = per-frame candidate capacity before
  * the canonical sort, rounded up to a power of 2 (0 = max(max_pts, 16384)).
  * stream = hipStream_t or NULL. */
 int surfhip_detector_create(surfhip_detector** det, const surfhip_param* param,
@@ -181,7 +183,10 @@ int surfhip_detector_geometry(surfhip_detector* det, int* iwhp /*3*/, int* swhp 
                               long long* ooff /*8*/, int* osize /*8*/);
 
 /* Stage-level entry points on frames already resident (parity tests and the
- * Hessian roofline run): integral only, Hessian only (needs integral). */
+ * Hessian roofline run): integral only, Hessian only.  run_hessian needs a
+ * prior run_integral (or detect_batch) on frames that are still live: the
+ * u8 Hessian kernels re-read those frames (SURFHIP_ERR_INVALID if there were
+ * none). */
 int surfhip_run_integral(surfhip_detector* det, const uint8_t* d_frames, int nframes,
                          int pitch, size_t frame_stride);
 int surfhip_run_hessian(surfhip_detector* det, int nframes);

@@ -219,4 +219,8 @@ def ref_host():
     L.ref_hessian_params.argtypes = [_i, _i, _i, _i, C.POINTER(_i), _i, _vp, _i, _i, _vp, _vp]
     L.ref_init_lut.argtypes = [_vp, _vp]
     L.ref_octave_plan.argtypes = [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]
+    L.ref_surfor_init.argtypes = [_vp, _i, C.c_float, _i, _i, _i, _i, _i, _i, _i, _i]
+    L.ref_alloc_geometry.restype = _i
+    L.ref_alloc_geometry.argtypes = [_i, _i, _i, _i, _i, _i, _vp, _vp, _vp]
+    L.ref_nms_grid.argtypes = [_i, _vp, _i, _i, _vp, _vp]
     return L

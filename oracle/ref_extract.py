@@ -17,6 +17,13 @@ three pieces of it are plain host C++ that g++ compiles as they stand:
                         recurrence and compute border1 (octave 0 / octaves > 0);
                         the harness runs them in surf.cpp:241-293's loop order
                         around cuCalcHessianMulti's parameter block
+  * surf.cpp:67-79      Surfor::init's SurfParam derivation (and whp)
+  * surf.cpp:377-392    allocMemory's geometry (iwhp, swhps, osizes, tot_osize)
+  * cuda_utils.h:160-163  iAlignUp, which both of the above call
+  * surfd.cu:3060-3076  cuFindMaximumWithInterp's NMS borders (mborders) and
+                        grid extent; the dim3 grid's three argument expressions
+                        are taken as text and evaluated into ints (no CUDA type
+                        is stood in for)
 
 The text is copied verbatim from /root/reference at build time into
 oracle/_ref/ (git-ignored) and wrapped in extern "C" harness functions whose
@@ -89,6 +96,46 @@ def extract_host():
             "where": (l1 + 1, l2 + 1, m + 1, bo + 1, b0 + 1)}
 
 
+def extract_more():
+    """surf.cpp Surfor::init / allocMemory, cuda_utils.h iAlignUp, surfd.cu's
+    NMS border loop and grid extent."""
+    cpp = open(os.path.join(REF, "surf.cpp")).read().split("\n")
+    cu = open(os.path.join(REF, "surfd.cu")).read().split("\n")
+    cuh = open(os.path.join(REF, "cuda_utils.h")).read().split("\n")
+    a = _find(cuh, "inline int iAlignUp(const int a, const int b)")
+    align, _ = _block(cuh, a)
+    si = _find(cpp, "void Surfor::init(")
+    i0 = _find(cpp, "whp.x = _width;", si)
+    i1 = _find(cpp, "its.nfeatures = _desc_wsz * _desc_wsz * its.orient_size;", i0)
+    init = cpp[i0:i1 + 1]
+    am = _find(cpp, "int Surfor::allocMemory(")
+    g0 = _find(cpp, "iwhp.x = its.doubled ? w + w - 1 : w + 1;", am)
+    lp = _find(cpp, "for (int i = 0, j = 1; j < its.noctaves; i++, j++)", g0)
+    loop, g1 = _block(cpp, lp)
+    geo = cpp[g0:g1 + 1]
+    fm = _find(cu, "void cuFindMaximumWithInterp(")
+    dx = _find(cu, "#define DX 16", fm)
+    dy = _find(cu, "#define DY 16", fm)
+    n0 = _find(cu, "int n = 0, b = 0, maxw = 0, maxh = 0;", fm)
+    nl = _find(cu, "for (int k = 1; k < its.max_scale - 1; k += 2)", n0)
+    nloop, _ = _block(cu, nl)
+    gr = _find(cu, "dim3 grid(", nl)
+    gline = cu[gr].strip()
+    assert gline.startswith("dim3 grid(") and gline.endswith(");"), gline
+    args, depth, cur = [], 0, ""
+    for ch in gline[len("dim3 grid("):-2]:
+        if ch == "," and depth == 0:
+            args.append(cur.strip()); cur = ""; continue
+        depth += ch == "("
+        depth -= ch == ")"
+        cur += ch
+    args.append(cur.strip())
+    assert len(args) == 3, args
+    return {"align": align, "init": init, "geo": geo,
+            "nms": [cu[dx], cu[dy], cu[n0], cu[n0 + 1]] + nloop, "grid": args,
+            "where": (a + 1, i0 + 1, i1 + 1, g0 + 1, g1 + 1, dx + 1, gr + 1)}
+
+
 HARNESS_HEAD = r'''// GENERATED by oracle/ref_extract.py from /root/reference (test infrastructure).
 #include <algorithm>
 #include <cmath>
@@ -154,6 +201,38 @@ def write_source(path):
     src.append("\t\toctave += octave;")
     src.append("\t}")
     src.append("}")
+    more = extract_more()
+    w2 = more["where"]
+    src.append(f"// cuda_utils.h:{w2[0]}")
+    src += more["align"]
+    src.append("struct ref_param { bool doubled; int noctaves; float divisor; int init_lobe; int max_scale; "
+               "int sampling; float thresh; bool upright; bool extend; int desc_wsz; int mag_factor; "
+               "int orient_size; int nfeatures; };")
+    src.append(f"// surf.cpp:{w2[1]}-{w2[2]} (Surfor::init)")
+    src.append("void surfor_init(ref_param& its, ref_dims& whp, const int _noctaves, const float _thresh, "
+               "const bool _doubled, const int _init_mask_size, const int _sampling_step, const bool _upright, "
+               "const bool _extend, const int _desc_wsz, const int _width, const int _height)")
+    src.append("{")
+    src += more["init"]
+    src.append("}")
+    src.append(f"// surf.cpp:{w2[3]}-{w2[4]} (allocMemory's geometry)")
+    src.append("int alloc_geometry(const ref_param& its, const int w, const int h, ref_dims& iwhp, ref_dims* swhps, "
+               "int* osizes)")
+    src.append("{")
+    src += more["geo"]
+    src.append("\treturn tot_osize;")
+    src.append("}")
+    src.append(f"// surfd.cu:{w2[5]}-{w2[6]} (cuFindMaximumWithInterp: NMS borders and grid)")
+    src.append("void nms_grid(const ref_param& its, const int* borders, ref_dims whp, int* mborders_out, int* grid_out)")
+    src.append("{")
+    src += more["nms"]
+    for k, e in enumerate(more["grid"]):
+        src.append(f"\tgrid_out[{k}] = {e};")
+    src.append("\tstd::memcpy(mborders_out, mborders, sizeof(mborders));")
+    src.append("\t(void)b;")
+    src.append("#undef DX")
+    src.append("#undef DY")
+    src.append("}")
     src.append("}  // namespace surfref")
     src.append(r'''
 extern "C" {
@@ -185,6 +264,47 @@ void ref_octave_plan(int init_lobe, int sampling, int noctaves, int max_scale, c
 {
     surfref::ref_its its = {init_lobe, sampling};
     surfref::octave_plan(its, noctaves, max_scale, swx, swy, borders, params, norms);
+}
+// Surfor::init: out = {doubled, noctaves, divisor (bits), init_lobe, max_scale,
+// sampling, thresh (bits), upright, extend, desc_wsz, mag_factor, orient_size,
+// nfeatures, whp.x, whp.y, whp.z}
+void ref_surfor_init(int* out, int noctaves, float thresh, int doubled, int init_mask_size, int sampling_step,
+                     int upright, int extend, int desc_wsz, int width, int height)
+{
+    surfref::ref_param its = {};
+    surfref::ref_dims whp = {};
+    surfref::surfor_init(its, whp, noctaves, thresh, doubled != 0, init_mask_size, sampling_step, upright != 0,
+                         extend != 0, desc_wsz, width, height);
+    int v[16] = {its.doubled, its.noctaves, 0, its.init_lobe, its.max_scale, its.sampling, 0, its.upright,
+                 its.extend, its.desc_wsz, its.mag_factor, its.orient_size, its.nfeatures, whp.x, whp.y, whp.z};
+    std::memcpy(&v[2], &its.divisor, 4);
+    std::memcpy(&v[6], &its.thresh, 4);
+    std::memcpy(out, v, sizeof(v));
+}
+// allocMemory's geometry: iwhp[3], swhps[3 * MAX_OCTAVE], osizes[MAX_OCTAVE]; returns tot_osize
+int ref_alloc_geometry(int doubled, int sampling, int max_scale, int noctaves, int w, int h, int* iwhp3,
+                       int* swhps3, int* osizes)
+{
+    surfref::ref_param its = {};
+    its.doubled = doubled != 0;
+    its.sampling = sampling;
+    its.max_scale = max_scale;
+    its.noctaves = noctaves;
+    surfref::ref_dims iwhp = {}, swhps[MAX_OCTAVE] = {};
+    const int tot = surfref::alloc_geometry(its, w, h, iwhp, swhps, osizes);
+    iwhp3[0] = iwhp.x; iwhp3[1] = iwhp.y; iwhp3[2] = iwhp.z;
+    for (int o = 0; o < MAX_OCTAVE; o++) {
+        swhps3[3 * o] = swhps[o].x; swhps3[3 * o + 1] = swhps[o].y; swhps3[3 * o + 2] = swhps[o].z;
+    }
+    return tot;
+}
+// NMS borders and grid extent of one octave (grid in blocks of DX x DY threads)
+void ref_nms_grid(int max_scale, const int* borders, int swx, int swy, int* mborders, int* grid3)
+{
+    surfref::ref_param its = {};
+    its.max_scale = max_scale;
+    surfref::ref_dims whp = {swx, swy, 0};
+    surfref::nms_grid(its, borders, whp, mborders, grid3);
 }
 void ref_hessian_params(int swx, int swy, int init_scale, int max_scale, int* init_mask_size, int init_border,
                         int* borders, int octave, int sampling, int* params_out, float* norms_out)

@@ -270,3 +270,49 @@ def test_wide_frames(surf, orc, w, h, batch):
         o_pts, o_desc, nc = orc.detect(op, frames[f], w, h)
         assert len(o_pts) > 100
         compare_frame(res["pts"][f], res["desc"][f], o_pts, o_desc, True)
+
+
+def test_wide_frame_tight_pitch(surf, orc):
+    """a wide frame (integral's 32-columns-per-thread path) with
+    the smallest legal pitch, align16(W) with W % 32 in (0, 16]: the last
+    16-byte half of a lane's 32 columns lies past the row (past the buffer on
+    the last row) and must not be read.  The frames sit at the very end of a
+    tight device buffer; integral bit-exact against the oracle."""
+    w, h, n = 5000, 96, 2
+    pitch = (w + 15) & ~15                     # 5008: 5000 % 32 = 8
+    assert pitch % 32 == 16
+    frames = surf.synth_frames(n, w, h, pitch=pitch, first=41)
+    param = surf.make_param(4, 4.0, upright=True)
+    det = surf.Detector(param, w, h, max_batch=n, max_pts=1024)
+    fb = surf.DeviceBuffer(frames.nbytes)
+    fb.upload(frames)
+    det.run_integral(fb.ptr, n, pitch, h * pitch)
+    surf.synchronize()
+    ii, iis, _, _ = det.workspace()
+    got = surf.download_ptr(ii, np.int32, n * iis).reshape(n, -1)
+    for f in range(n):
+        ii_ref = orc.integral(frames[f], w, h)
+        ip = ii_ref.shape[1]
+        assert np.array_equal(got[f][: (h + 1) * ip].reshape(h + 1, ip)[:, : w + 1], ii_ref[:, : w + 1]), f
+    det.close()
+
+
+def test_detector_rejects_oversized_grids(surf):
+    """octave-0 sample grids past the NMS record fields (14-bit
+    row / column, 13-bit block row) are rejected at creation instead of
+    silently corrupting the candidate order."""
+    param = surf.make_param(4, 4.0, upright=True, sampling_step=1)
+    with pytest.raises(surf.SurfError):
+        surf.Detector(param, 64, 16400, max_batch=1, max_pts=64)
+    ok = surf.Detector(param, 64, 4000, max_batch=1, max_pts=64)
+    ok.close()
+
+
+def test_run_hessian_without_integral(surf):
+    """run_hessian before any run_integral is an argument error
+    (the u8 Hessian kernels would have no frames), not a HIP error."""
+    param = surf.make_param(4, 4.0, upright=True)
+    det = surf.Detector(param, 1920, 1080, max_batch=16, max_pts=1024)
+    with pytest.raises(surf.SurfError, match="invalid argument"):
+        det.run_hessian(16)
+    det.close()

@@ -558,3 +558,27 @@ def test_ingest_ring_equals_resident_batches(surf, depth, upright, extend, tmp_p
         assert p.tobytes() == p0.tobytes() and d.tobytes() == d0.tobytes()
     ing.close()
     det.close()
+
+
+@pytest.mark.parametrize("w,h,mask,st,doubled,noct", [(1920, 1080, 9, 2, False, 4), (640, 480, 9, 2, True, 5),
+                                                       (321, 241, 6, 1, False, 6), (3840, 2160, 12, 3, False, 4)])
+def test_detector_geometry_pinned_to_reference_alloc_memory(surf, orc, w, h, mask, st, doubled, noct):
+    """The product's derive() (surfhip_detector_geometry) against allocMemory's
+    own statements (surf.cpp:377-392, compiled from the reference into
+    oracle/_ref by oracle/ref_extract.py): iwhp, swhps and osizes."""
+    L = orc.ref_host()
+    if L is None:
+        pytest.skip("oracle/_ref not built (no reference sources when it was built)")
+    p = orc.make_param(noct, 4.0, doubled, mask, st, True, False, 4)
+    iwhp = np.zeros(3, np.int32)
+    sw = np.zeros(3 * 8, np.int32)
+    osz = np.zeros(8, np.int32)
+    L.ref_alloc_geometry(int(doubled), p.sampling, p.max_scale, noct, w, h, iwhp.ctypes.data, sw.ctypes.data,
+                         osz.ctypes.data)
+    param = surf.make_param(noct, 4.0, doubled=doubled, init_mask_size=mask, sampling_step=st, upright=True)
+    det = surf.Detector(param, w, h, max_batch=1, max_pts=64)
+    giw, gsw, _, gos = det.geometry()
+    det.close()
+    assert giw == tuple(iwhp)
+    for o in range(noct):
+        assert gsw[o] == tuple(sw[3 * o:3 * o + 3]) and gos[o] == osz[o], o

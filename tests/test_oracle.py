@@ -704,3 +704,75 @@ def test_descriptor_quotient_matches_ieee_division(orc):
     fn.restype = C.c_long
     fn.argtypes = [C.c_long, C.c_uint64]
     assert fn(20_000_000, 12345) == 0
+
+
+# Surfor::init (surf.cpp:67-79), allocMemory's geometry (surf.cpp:377-392 with
+# cuda_utils.h:160-163 iAlignUp) and cuFindMaximumWithInterp's NMS borders and
+# grid (surfd.cu:3060-3076), compiled from the reference as they stand.
+
+_INIT_CASES = [(m, st, d, u, e, wsz) for m in range(6, 21) for st in (1, 2, 3) for d in (False, True)
+               for u, e in ((True, False), (False, True)) for wsz in (1, 2, 3, 4, 5, 6, 7)]
+
+
+def _ref_init(L, noct, thresh, doubled, mask, st, upright, extend, wsz, w=1920, h=1080):
+    v = np.zeros(16, np.int32)
+    L.ref_surfor_init(v.ctypes.data, noct, thresh, int(doubled), mask, st, int(upright), int(extend), wsz, w, h)
+    f = v.view(np.float32)
+    return {"doubled": bool(v[0]), "noctaves": int(v[1]), "divisor": f[2], "init_lobe": int(v[3]),
+            "max_scale": int(v[4]), "sampling": int(v[5]), "thresh": f[6], "upright": bool(v[7]),
+            "extend": bool(v[8]), "desc_wsz": int(v[9]), "mag_factor": int(v[10]),
+            "orient_size": int(v[11]), "nfeatures": int(v[12]), "whp": (int(v[13]), int(v[14]), int(v[15]))}
+
+
+def test_param_derivation_pinned_to_reference_init(orc, surf):
+    """Every SurfParam field the oracle (or_init_param) and the product
+    (surfhip_make_param, host code of libsurfhip.so: no GPU call) derive,
+    against Surfor::init's own statements, over init masks 6-20, sampling
+    1-3, doubled, rotated/extended and desc_wsz 1-7; whp.z = iAlignUp(W, 128)
+    is the pitch the ingest ring and the bench use."""
+    L = _ref_or_skip(orc)
+    for mask, st, d, u, e, wsz in _INIT_CASES:
+        r = _ref_init(L, 4, 4.0, d, mask, st, u, e, wsz)
+        o = orc.make_param(4, 4.0, d, mask, st, u, e, wsz)
+        g = surf.make_param(4, 4.0, doubled=d, init_mask_size=mask, sampling_step=st, upright=u,
+                            extend=e, desc_wsz=wsz)
+        for name in ("doubled", "noctaves", "init_lobe", "max_scale", "sampling", "upright", "extend",
+                     "desc_wsz", "mag_factor", "orient_size", "nfeatures"):
+            assert getattr(o, name) == r[name] == getattr(g, name), (name, mask, st, d, u, e, wsz)
+        for name in ("divisor", "thresh"):
+            want = np.float32(r[name]).tobytes()
+            assert np.float32(getattr(o, name)).tobytes() == want == np.float32(getattr(g, name)).tobytes()
+    assert r["whp"] == (1920, 1080, surf.align_up(1920, 128))
+
+
+@pytest.mark.parametrize("w,h", [(640, 480), (1920, 1080), (3840, 2160), (321, 241), (1281, 961), (64, 48)])
+@pytest.mark.parametrize("mask,st,doubled,noct", [(9, 2, False, 4), (9, 2, True, 5), (6, 1, False, 6),
+                                                   (12, 3, False, 4), (18, 2, True, 4), (15, 1, True, 3)])
+def test_geometry_pinned_to_reference_alloc_memory(orc, w, h, mask, st, doubled, noct):
+    """or_geometry's iwhp / swhps / osizes / tot_osize against allocMemory's
+    own statements (the product's derive() is checked against the same
+    reference values on the GPU: test_gpu_parity.py), and the oracle's NMS
+    start offsets and launch extent against cuFindMaximumWithInterp's."""
+    L = _ref_or_skip(orc)
+    p = orc.make_param(noct, 4.0, doubled, mask, st, True, False, 4)
+    g, octs = orc.geometry(p, w, h)
+    iwhp = np.zeros(3, np.int32)
+    sw = np.zeros(3 * 8, np.int32)
+    osz = np.zeros(8, np.int32)
+    tot = L.ref_alloc_geometry(int(doubled), p.sampling, p.max_scale, noct, w, h, iwhp.ctypes.data,
+                               sw.ctypes.data, osz.ctypes.data)
+    assert (g.iwhp.x, g.iwhp.y, g.iwhp.z) == tuple(iwhp)
+    assert g.tot_osize == tot
+    for o in range(noct):
+        assert (g.swhp[o].x, g.swhp[o].y, g.swhp[o].z) == tuple(sw[3 * o:3 * o + 3]), o
+        assert g.osize[o] == osz[o], o
+        q = octs[o]
+        mb = np.zeros(3, np.int32)
+        grid = np.zeros(3, np.int32)
+        borders = np.array(list(q.borders), np.int32)
+        L.ref_nms_grid(p.max_scale, borders.ctypes.data, g.swhp[o].x, g.swhp[o].y, mb.ctypes.data, grid.ctypes.data)
+        nlev = int(grid[2])
+        assert nlev == len(range(1, p.max_scale - 1, 2))
+        assert list(q.mborders)[:nlev] == mb[:nlev].tolist(), o
+        # the oracle keeps the extent in threads (DX = DY = 16 per block)
+        assert (q.nms_gx, q.nms_gy) == (int(grid[0]) * 16, int(grid[1]) * 16), o
