@@ -228,6 +228,10 @@ def main():
                     help="fixed per-rank slab capacity = max over ranks of the warm-up slab x this")
     ap.add_argument("--no-exchange-probe", action="store_true",
                     help="N = 1: skip the 1-rank RCCL all-gather of the real slab")
+    ap.add_argument("--exchange-proxy", type=int, default=0, metavar="N",
+                    help="N = 1 only: after the timed region, time the step again with the HBM traffic an N-rank "
+                         "all-gather would put on this GPU each step ((N-1) x slab bytes copied D2D on a comm "
+                         "stream beside compute), for --gather full and points (SURVEY 8e; DESIGN.md 5)")
     ap.add_argument("--cpu-frames", type=int, default=128, help="frames per CPU baseline chunk")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline wall-time budget")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -387,6 +391,11 @@ def run_rank(args):
     torch.cuda.synchronize(dev)
 
     timing[0] = True
+    # the Hessian launches of every timed step, bracketed by HIP events on the
+    # detector's stream in their pipelined arrangement (the integral runs
+    # beside them on the side stream): the roofline's launch time
+    if not args.hessian_only:
+        det.time_hessian(True)
     t_start = time.perf_counter()
     for i in range(args.steps):
         step()
@@ -396,6 +405,8 @@ def run_rank(args):
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
     timing[0] = False
+    hess_instep = det.hessian_times() if not args.hessian_only else []
+    det.time_hessian(False)
     if world > 1:
         elapsed = float(allreduce_max(elapsed, torch.float64))
 
@@ -472,7 +483,8 @@ def run_rank(args):
         det.set_profiling(False)
         torch.cuda.synchronize(dev)
     # the Hessian stage alone (events on the detector's stream; all its
-    # kernels in series), after one integral of the same frames
+    # kernels in series, nothing beside them), after one integral of the same
+    # frames: the serial figure, reported next to the in-step one
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     if not args.hessian_only:
@@ -482,7 +494,8 @@ def run_rank(args):
         det.run_hessian(B)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    hess_ms = ev0.elapsed_time(ev1) / args.steps
+    hess_serial_ms = ev0.elapsed_time(ev1) / args.steps
+    hess_ms = float(np.mean(hess_instep)) if hess_instep else hess_serial_ms
 
     # N = 1: what this rank's exchange would move -- a 1-rank RCCL all-gather
     # (libsurfcomm) of the real slab, both modes, after the timed region
@@ -490,6 +503,11 @@ def run_rank(args):
     if world == 1 and not args.hessian_only and not args.no_exchange_probe:
         with _StdoutToStderr():
             probe = exchange_probe(surf, torch, det, dev, stream, d_pts, d_desc, d_cnt, B, nf)
+
+    proxy = None
+    if world == 1 and args.exchange_proxy > 1 and not args.hessian_only:
+        proxy = exchange_proxy(torch, det, dev, stream, run_batch, d_pts, d_desc, d_cnt, B, args.exchange_proxy,
+                               args.steps, 1e3 * elapsed / args.steps)
 
     frames_total = world * B * args.steps
     value = frames_total / elapsed
@@ -522,18 +540,30 @@ def run_rank(args):
             "keypoints_per_frame": round(kp_total_batch / (world * B), 1),
             "keypoints_per_step": kp_total_batch,
             "stage_ms_per_step_serial": {k: round(v / nprof, 4) for k, v in stage_acc.items()},
-            "roofline": {"kernel": "Hessian stage, all octaves in series: " + det.hessian_kernels() + ", per batch",
-                         "bound": "hbm",
+            "roofline": {"kernel": "Hessian stage, all octaves: " + det.hessian_kernels() + ", per batch",
+                         # what the counters say limits it: VALU
+                         # issue and latency, not HBM; `frac` is still priced
+                         # against the HBM peak, as SURVEY 8(d) defines it
+                         "bound": "valu-issue",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_profile": traffic_tag,
-                         "algorithmic_bytes_per_launch": hb, "launch_ms": round(hess_ms, 4)},
+                         # the counter bytes (what the kernels really move) over the same time
+                         "frac_traffic": (None if not traffic else
+                                          round(traffic / (hess_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)),
+                         "algorithmic_bytes_per_launch": hb, "launch_ms": round(hess_ms, 4),
+                         "launch_ms_source": ("in-step: HIP events around the Hessian launches of each timed "
+                                              f"step ({len(hess_instep)} steps), integral beside them"
+                                              if hess_instep else "serial"),
+                         "launch_ms_serial": round(hess_serial_ms, 4)},
             "gen_s": round(gen_s, 2),
         }
         if exchanged is not None:
             result["exchange"] = exchanged
         elif probe is not None:
             result["exchange"] = probe
+        if proxy is not None:
+            result["exchange_proxy"] = proxy
         if world == 1 and not args.no_cpu and not args.hessian_only:
             result["cpu_baseline"] = cpu_baseline(frames, W, H, args)
         else:
@@ -563,6 +593,65 @@ class _StdoutToStderr:
         os.dup2(self.saved, 1)
         os.close(self.saved)
         return False
+
+
+def exchange_proxy(torch, det, dev, stream, run_batch, d_pts, d_desc, d_cnt, B, nranks, steps, base_ms):
+    """Single-GPU proxy of the N-rank exchange's cost to the step: each step
+    packs its slab (as the N > 1 loop does) and a comm stream then writes
+    (N-1) x slab bytes into a receive buffer by a D2D copy -- the bytes an
+    all-gather lands in this GPU's HBM -- beside the next batch's compute
+    (gather(i) overlaps compute(i+1), as in the real loop).  xGMI link time is
+    not in it (DESIGN.md 5 models that); what it measures is the HBM and CU
+    contention the received slabs cost the pipeline."""
+    out = {"nranks": nranks, "base_ms_per_step": round(base_ms, 4),
+           "note": "D2D copy of (N-1) x slab bytes per step on a comm stream, event-ordered after the pack; "
+                   "the xGMI transfer itself is modelled in DESIGN.md 5"}
+    total = det.batch_total(B)
+    cs = torch.cuda.Stream(dev)
+    for mode in ("full", "points"):
+        used = det.slab_bytes(B, total, desc=mode == "full")
+        cap = (int(used * 1.10) + 64 + 255) // 256 * 256
+        slab = [torch.empty(cap, dtype=torch.uint8, device=dev) for _ in range(2)]
+        src = torch.empty((nranks - 1) * cap, dtype=torch.uint8, device=dev)
+        dst = [torch.empty((nranks - 1) * cap, dtype=torch.uint8, device=dev) for _ in range(2)]
+        src.fill_(1)
+        packed = [torch.cuda.Event() for _ in range(2)]
+        landed = [torch.cuda.Event() for _ in range(2)]
+        cev = []
+
+        def one(i, timed):
+            k = i & 1
+            run_batch()
+            if i >= 2:
+                stream.wait_event(landed[k])
+            det.pack_slab_cap(d_pts.data_ptr(), d_desc.data_ptr() if mode == "full" else None, d_cnt.data_ptr(),
+                              B, slab[k].data_ptr(), cap)
+            packed[k].record(stream)
+            cs.wait_event(packed[k])
+            with torch.cuda.stream(cs):
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if timed else None
+                if ev:
+                    ev[0].record(cs)
+                dst[k].copy_(src, non_blocking=True)
+                if ev:
+                    ev[1].record(cs)
+                    cev.append(ev)
+            landed[k].record(cs)
+
+        for i in range(3):
+            one(i, False)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            one(3 + i, True)
+        torch.cuda.synchronize(dev)
+        ms = 1e3 * (time.perf_counter() - t0) / steps
+        cms = float(np.mean([a.elapsed_time(b) for a, b in cev]))
+        out[mode] = {"slab_bytes": used, "received_bytes_per_step": (nranks - 1) * cap,
+                     "ms_per_step": round(ms, 4), "copy_ms": round(cms, 4),
+                     "slowdown": round(ms / base_ms, 4)}
+        del slab, src, dst
+    return out
 
 
 def exchange_probe(surf, torch, det, dev, stream, d_pts, d_desc, d_cnt, B, nf, reps=5):

@@ -110,6 +110,8 @@ _sigs = {
     "surfhip_detector_capacity": (_i, [_vp, C.POINTER(_i)]),
     "surfhip_detector_set_profiling": (_i, [_vp, _i]),
     "surfhip_detector_stage_times": (_i, [_vp, C.POINTER(C.c_float)]),
+    "surfhip_detector_time_hessian": (_i, [_vp, _i]),
+    "surfhip_detector_hessian_times": (_i, [_vp, C.POINTER(C.c_float), _i, C.POINTER(_i)]),
     "surfhip_detector_workspace": (_i, [_vp, C.POINTER(_vp), C.POINTER(_sz), C.POINTER(_vp), C.POINTER(_sz)]),
     "surfhip_detector_geometry": (_i, [_vp, C.POINTER(_i), C.POINTER(_i), C.POINTER(C.c_longlong), C.POINTER(_i)]),
     "surfhip_run_integral": (_i, [_vp, _vp, _i, _i, _sz]),
@@ -269,6 +271,18 @@ class Detector:
 
     def set_profiling(self, on: bool) -> None:
         check(_lib.surfhip_detector_set_profiling(self.h, int(on)), "set_profiling")
+
+    def time_hessian(self, on: bool) -> None:
+        """Record the Hessian launches of the following batches with HIP events
+        in their in-step (pipelined) arrangement."""
+        check(_lib.surfhip_detector_time_hessian(self.h, int(on)), "time_hessian")
+
+    def hessian_times(self) -> list:
+        """Milliseconds of each recorded batch's Hessian launches (and reset)."""
+        ms = (C.c_float * 64)()
+        n = _i(0)
+        check(_lib.surfhip_detector_hessian_times(self.h, ms, 64, C.byref(n)), "hessian_times")
+        return [float(ms[k]) for k in range(n.value)]
 
     def stage_times(self) -> dict:
         ms = (C.c_float * NSTAGE)()

@@ -84,6 +84,9 @@ struct surfhip_detector {
     hipStream_t side = nullptr;         // integral + integral-image Hessian kernels, beside the u8 ones
     hipEvent_t fork = nullptr, join = nullptr;
     float stage_ms[SURFHIP_NSTAGE]{};
+    bool time_hess = false;             // in-step Hessian event pairs (surfhip_detector_time_hessian)
+    hipEvent_t hev[SURFHIP_MAX_HESS_EV][2]{};
+    int hev_n = 0;
     int last_nframes = 0;
     const uint8_t* last_frames = nullptr;   // u8 source of the last integral (surfhip_run_hessian)
     int last_pitch = 0;
@@ -405,6 +408,9 @@ static void free_all(surfhip_detector* d)
         if (p) (void)hipFree(p);
     for (int i = 0; i < SURFHIP_NSTAGE; i++)
         if (d->ev[i]) (void)hipEventDestroy(d->ev[i]);
+    for (int i = 0; i < SURFHIP_MAX_HESS_EV; i++)
+        for (int j = 0; j < 2; j++)
+            if (d->hev[i][j]) (void)hipEventDestroy(d->hev[i][j]);
     if (d->fork) (void)hipEventDestroy(d->fork);
     if (d->join) (void)hipEventDestroy(d->join);
     if (d->side) (void)hipStreamDestroy(d->side);
@@ -613,8 +619,11 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
         HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
                               d->plan, d->side, 2));
         HIPCHK(hipEventRecord(d->join, d->side));
+        const bool th = d->time_hess && d->hev_n < SURFHIP_MAX_HESS_EV;
+        if (th) HIPCHK(hipEventRecord(d->hev[d->hev_n][0], s));
         HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
                               d->plan, s, 1));
+        if (th) HIPCHK(hipEventRecord(d->hev[d->hev_n++][1], s));
         HIPCHK(hipStreamWaitEvent(s, d->join, 0));
     }
     HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->scan_key, d->scan_src, d->scan_cube,
@@ -703,6 +712,32 @@ int surfhip_detector_stage_times(surfhip_detector* d, float* ms)
     HIPCHK(hipEventSynchronize(d->ev[SURFHIP_NSTAGE - 1]));
     for (int i = 0; i < SURFHIP_NSTAGE - 1; i++) HIPCHK(hipEventElapsedTime(&ms[i], d->ev[i], d->ev[i + 1]));
     HIPCHK(hipEventElapsedTime(&ms[SURFHIP_NSTAGE - 1], d->ev[0], d->ev[SURFHIP_NSTAGE - 1]));
+    return SURFHIP_OK;
+}
+
+int surfhip_detector_time_hessian(surfhip_detector* d, int on)
+{
+    if (!d) return SURFHIP_ERR_INVALID;
+    if (on) {
+        for (int i = 0; i < SURFHIP_MAX_HESS_EV; i++)
+            for (int j = 0; j < 2; j++)
+                if (!d->hev[i][j]) HIPCHK(hipEventCreate(&d->hev[i][j]));
+    }
+    d->time_hess = on != 0;
+    d->hev_n = 0;
+    return SURFHIP_OK;
+}
+
+int surfhip_detector_hessian_times(surfhip_detector* d, float* ms, int max, int* n)
+{
+    if (!d || !n || (max > 0 && !ms)) return SURFHIP_ERR_INVALID;
+    const int k = std::min(d->hev_n, std::max(max, 0));
+    for (int i = 0; i < k; i++) {
+        HIPCHK(hipEventSynchronize(d->hev[i][1]));
+        HIPCHK(hipEventElapsedTime(&ms[i], d->hev[i][0], d->hev[i][1]));
+    }
+    *n = k;
+    d->hev_n = 0;
     return SURFHIP_OK;
 }
 

@@ -173,6 +173,16 @@ int surfhip_detector_capacity(surfhip_detector* det, int* cand_cap);
 int surfhip_detector_set_profiling(surfhip_detector* det, int on);
 int surfhip_detector_stage_times(surfhip_detector* det, float* ms);
 
+/* In-step Hessian timing: with `on`, every following detect_batch records a
+ * HIP event pair on the detector's stream around its Hessian launches, in
+ * their normal (pipelined) arrangement -- the integral runs beside them on
+ * the side stream -- for up to SURFHIP_MAX_HESS_EV batches.
+ * surfhip_detector_hessian_times waits for them, writes the per-batch
+ * milliseconds to ms[0..*n) and starts a new record. */
+#define SURFHIP_MAX_HESS_EV 64
+int surfhip_detector_time_hessian(surfhip_detector* det, int on);
+int surfhip_detector_hessian_times(surfhip_detector* det, float* ms, int max, int* n);
+
 /* Workspace access for parity tests: device pointers to frame 0's integral
  * image ((H+1) x ipitch int32, frame stride ii_stride ints) and response
  * planes (resp_stride floats per frame; octave o plane s at
