@@ -228,6 +228,9 @@ def main():
                     help="fixed per-rank slab capacity = max over ranks of the warm-up slab x this")
     ap.add_argument("--no-exchange-probe", action="store_true",
                     help="N = 1: skip the 1-rank RCCL all-gather of the real slab")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="compute each batch's integral beside its own Hessian instead of beside the previous "
+                         "batch's describe (surfhip_detect_batch_next)")
     ap.add_argument("--exchange-proxy", type=int, default=0, metavar="N",
                     help="N = 1 only: after the timed region, time the step again with the HBM traffic an N-rank "
                          "all-gather would put on this GPU each step ((N-1) x slab bytes copied D2D on a comm "
@@ -309,9 +312,16 @@ def run_rank(args):
             if args.with_integral:
                 det.run_integral(d_frames.data_ptr(), B, pitch, H * pitch)
             det.run_hessian(B)
-        else:
+        elif args.no_pipeline:
             det.detect_batch(d_frames.data_ptr(), B, pitch, H * pitch, d_pts.data_ptr(), d_desc.data_ptr(),
                              d_cnt.data_ptr())
+            torch.maximum(d_cnt_max, d_cnt, out=d_cnt_max)
+        else:
+            # the next step's batch is the same resident frames: its integral
+            # is computed beside this batch's describe (one integral per step,
+            # as in the serial arrangement)
+            det.detect_batch_next(d_frames.data_ptr(), B, pitch, H * pitch, d_pts.data_ptr(), d_desc.data_ptr(),
+                                  d_cnt.data_ptr(), d_frames.data_ptr(), B, pitch, H * pitch)
             torch.maximum(d_cnt_max, d_cnt, out=d_cnt_max)
 
     if args.hessian_only:

@@ -104,6 +104,7 @@ _sigs = {
     "surfhip_detector_set_stream": (_i, [_vp, _vp]),
     "surfhip_make_param": (_i, [C.POINTER(SurfParam), _i, C.c_float, _i, _i, _i, _i, _i, _i]),
     "surfhip_detect_batch": (_i, [_vp, _vp, _i, _i, _sz, _vp, _vp, _vp]),
+    "surfhip_detect_batch_next": (_i, [_vp, _vp, _i, _i, _sz, _vp, _vp, _vp, _vp, _i, _i, _sz]),
     "surfhip_detect": (_i, [_vp, _vp, _i, _vp, _i, C.POINTER(_i), C.POINTER(_vp), _i]),
     "surfhip_detector_candidates": (_i, [_vp, C.POINTER(_i), _i]),
     "surfhip_detector_status": (_i, [_vp, C.POINTER(_i)]),
@@ -293,6 +294,15 @@ class Detector:
                      points_ptr: int, desc_ptr: int | None, counts_ptr: int) -> None:
         check(_lib.surfhip_detect_batch(self.h, frames_ptr, nframes, pitch, stride, points_ptr,
                                         desc_ptr, counts_ptr), "detect_batch")
+
+    def detect_batch_next(self, frames_ptr: int, nframes: int, pitch: int, stride: int, points_ptr: int,
+                          desc_ptr: int | None, counts_ptr: int, next_ptr: int | None, next_nframes: int = 0,
+                          next_pitch: int = 0, next_stride: int = 0) -> None:
+        """detect_batch, with the next batch's integral computed beside this
+        batch's describe stage (surfhip_detect_batch_next)."""
+        check(_lib.surfhip_detect_batch_next(self.h, frames_ptr, nframes, pitch, stride, points_ptr, desc_ptr,
+                                             counts_ptr, next_ptr, next_nframes, next_pitch, next_stride),
+              "detect_batch_next")
 
     def run_integral(self, frames_ptr, nframes, pitch, stride) -> None:
         check(_lib.surfhip_run_integral(self.h, frames_ptr, nframes, pitch, stride), "run_integral")

@@ -59,7 +59,15 @@ struct surfhip_detector {
     long long dstride = 0;
     int nbands = 0, CW = 0;
     size_t tot_osize = 0;
-    int32_t* ii = nullptr;
+    int32_t* ii = nullptr;              // integral of the last processed batch (one of iib)
+    int32_t* iib[2] = {nullptr, nullptr};   // integral buffers: the batch's, and the next batch's prefetch
+    int icur = 0;                       // iib index of ii
+    // prefetched integral (surfhip_detect_batch_next): which frames, in iib[ipref]
+    bool pref_valid = false;
+    int ipref = 0, pref_n = 0, pref_pitch = 0;
+    const uint8_t* pref_frames = nullptr;
+    size_t pref_stride = 0;
+    hipEvent_t fork2 = nullptr;
     float* resp = nullptr;
     uint32_t* colsum = nullptr;
     surfhip_point* cand = nullptr;
@@ -401,7 +409,7 @@ static int derive(surfhip_detector* d)
 
 static void free_all(surfhip_detector* d)
 {
-    void* ptrs[] = {d->d_oct, d->ii, d->resp, d->colsum, d->cand, d->keys, d->gscratch, d->cand_count,
+    void* ptrs[] = {d->d_oct, d->iib[0], d->iib[1], d->resp, d->colsum, d->cand, d->keys, d->gscratch, d->cand_count,
                     d->scan_key, d->scan_src, d->scan_cube, d->item_count, d->item_off,
                     d->offsets, d->order, d->status, d->pts1, d->desc1, d->count1, d->dbl};
     for (void* p : ptrs)
@@ -412,6 +420,7 @@ static void free_all(surfhip_detector* d)
         for (int j = 0; j < 2; j++)
             if (d->hev[i][j]) (void)hipEventDestroy(d->hev[i][j]);
     if (d->fork) (void)hipEventDestroy(d->fork);
+    if (d->fork2) (void)hipEventDestroy(d->fork2);
     if (d->join) (void)hipEventDestroy(d->join);
     if (d->side) (void)hipStreamDestroy(d->side);
 }
@@ -467,7 +476,8 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     } while (0)
     make_plan(d->P, d->oct, d->plan, max_batch);
     ALLOC(d->d_oct, sizeof(OctaveParams) * kMaxOct);
-    ALLOC(d->ii, B * d->P.ii_stride * sizeof(int32_t));
+    ALLOC(d->iib[0], B * d->P.ii_stride * sizeof(int32_t));
+    d->ii = d->iib[0];
     ALLOC(d->resp, B * d->tot_osize * sizeof(float));
     ALLOC(d->colsum, (size_t)integral_bands(d->H, B) * d->CW * sizeof(uint32_t));
     ALLOC(d->cand, B * d->cap * sizeof(surfhip_point));
@@ -496,7 +506,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     // zero once: integral pad columns and response pad columns are never
     // written by the kernels and never read by them either
     e = hipMemcpy(d->d_oct, d->oct, sizeof(OctaveParams) * kMaxOct, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemset(d->ii, 0, B * d->P.ii_stride * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemset(d->iib[0], 0, B * d->P.ii_stride * sizeof(int32_t));
     if (e == hipSuccess) e = hipMemset(d->resp, 0, B * d->tot_osize * sizeof(float));
     if (e == hipSuccess) e = hipMemset(d->status, 0, 16);
     if (e != hipSuccess) goto fail;
@@ -518,6 +528,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     e = hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&d->fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&d->join, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&d->fork2, hipEventDisableTiming);
     if (e != hipSuccess) goto fail;
     *out = d;
     return SURFHIP_OK;
@@ -532,6 +543,7 @@ int surfhip_detector_destroy(surfhip_detector* d)
 {
     if (!d) return SURFHIP_ERR_INVALID;
     (void)hipStreamSynchronize(d->stream);
+    if (d->side) (void)hipStreamSynchronize(d->side);    // a next-batch integral may still run there
     free_all(d);
     delete d;
     return SURFHIP_OK;
@@ -570,8 +582,12 @@ int surfhip_run_integral(surfhip_detector* d, const uint8_t* frames, int nframes
 {
     int rc = check_frames(d, frames, nframes, pitch, stride);
     if (rc) return rc;
+    // a prefetch on the side stream may still be using the colsum scratch
+    HIPCHK(hipEventRecord(d->join, d->side));
+    HIPCHK(hipStreamWaitEvent(d->stream, d->join, 0));
     HIPCHK(source_frames(d, frames, pitch, stride, nframes, d->stream));
     HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, d->stream));
+    d->pref_valid = false;
     d->last_frames = frames;
     d->last_pitch = pitch;
     d->last_fstride = (long long)stride;
@@ -588,14 +604,40 @@ int surfhip_run_hessian(surfhip_detector* d, int nframes)
     return SURFHIP_OK;
 }
 
-int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes, int pitch,
-                         size_t stride, surfhip_point* points, float* desc, int* counts)
+// The second integral buffer is allocated on first use of the pipelined
+// entry point (a plain detect_batch caller never pays for it).
+static hipError_t ensure_second_ii(surfhip_detector* d)
+{
+    if (d->iib[1]) return hipSuccess;
+    const size_t bytes = (size_t)d->max_batch * d->P.ii_stride * sizeof(int32_t);
+    hipError_t e = hipMalloc((void**)&d->iib[1], bytes);
+    if (e == hipSuccess) e = hipMemset(d->iib[1], 0, bytes);     // pad columns stay 0
+    return e;
+}
+
+int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nframes, int pitch, size_t stride,
+                              surfhip_point* points, float* desc, int* counts, const uint8_t* next_frames,
+                              int next_nframes, int next_pitch, size_t next_stride)
 {
     int rc = check_frames(d, frames, nframes, pitch, stride);
     if (rc) return rc;
     if (!points || !counts) return SURFHIP_ERR_INVALID;
+    // no prefetch for doubled frames (the upsampled frames share one scratch
+    // buffer) or while stage profiling (serial stages)
+    const bool pipe = next_frames != nullptr && !d->param.doubled && !d->profiling;
+    if (next_frames && !d->param.doubled) {
+        rc = check_frames(d, next_frames, next_nframes, next_pitch, next_stride);
+        if (rc) return rc;
+    }
+    if (pipe) HIPCHK(ensure_second_ii(d));
     hipStream_t s = d->stream;
     const bool prof = d->profiling;
+    // this batch's integral: prefetched by the previous call (same frames), or computed now
+    const bool have = !prof && d->pref_valid && d->pref_frames == frames && d->pref_n == nframes &&
+                      d->pref_pitch == pitch && d->pref_stride == stride;
+    d->icur = have ? d->ipref : d->icur;
+    d->ii = d->iib[d->icur];
+    d->pref_valid = false;
     HIPCHK(hipMemsetAsync(d->cand_count, 0, sizeof(int) * nframes, s));
     HIPCHK(hipMemsetAsync(d->status, 0, sizeof(int), s));       // per-batch truncation flag
     HIPCHK(hipMemsetAsync(d->item_count, 0, sizeof(int) * (size_t)nframes * d->nitems, s));
@@ -609,13 +651,14 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
                               d->plan, s));
         HIPCHK(hipEventRecord(d->ev[2], s));
     } else {
-        // the u8 Hessian kernels (octaves 0, 1) need no integral image: they run
-        // on s beside the integral and the integral-image Hessian kernels
-        // (octaves >= 2) on the side stream; s waits for both
+        // the u8 Hessian kernels need no integral image: they run on s; the
+        // integral (unless prefetched) and the integral-image Hessian kernels
+        // run on the side stream beside them; s waits for both before NMS
         HIPCHK(source_frames(d, frames, pitch, stride, nframes, s));
         HIPCHK(hipEventRecord(d->fork, s));
         HIPCHK(hipStreamWaitEvent(d->side, d->fork, 0));
-        HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, d->side));
+        if (!have)
+            HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, d->side));
         HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
                               d->plan, d->side, 2));
         HIPCHK(hipEventRecord(d->join, d->side));
@@ -633,15 +676,38 @@ int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes
     HIPCHK(launch_sort(d->cand, d->keys, d->gscratch, d->cand_count, d->item_off, d->plan.nms_start[kMaxOct] * 4,
                        d->cap, nframes, points, d->max_pts, counts, d->offsets, d->order, d->status, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[4], s));
+    if (pipe) {
+        // the next batch's integral, on the side stream beside this batch's
+        // describe (latency-bound gathers: HBM and issue slots to spare);
+        // ordered after everything on s so far, so the other buffer's last
+        // readers (the previous batch's fit and describe) are done
+        const int nx = d->icur ^ 1;
+        HIPCHK(hipEventRecord(d->fork2, s));
+        HIPCHK(hipStreamWaitEvent(d->side, d->fork2, 0));
+        HIPCHK(launch_integral(next_frames, next_pitch, (long long)next_stride, next_nframes, d->P, d->colsum,
+                               d->iib[nx], d->side));
+        d->pref_valid = true;
+        d->ipref = nx;
+        d->pref_frames = next_frames;
+        d->pref_n = next_nframes;
+        d->pref_pitch = next_pitch;
+        d->pref_stride = next_stride;
+    }
     if (desc)
         HIPCHK(launch_describe(d->ii, d->P, points, d->max_pts, counts, d->offsets, d->order, nframes, desc,
-                               d->status + 64, s));
+                               d->status + 64, s, pipe));
     if (prof) HIPCHK(hipEventRecord(d->ev[5], s));
     d->last_nframes = nframes;
     d->last_frames = frames;
     d->last_pitch = pitch;
     d->last_fstride = (long long)stride;
     return SURFHIP_OK;
+}
+
+int surfhip_detect_batch(surfhip_detector* d, const uint8_t* frames, int nframes, int pitch,
+                         size_t stride, surfhip_point* points, float* desc, int* counts)
+{
+    return surfhip_detect_batch_next(d, frames, nframes, pitch, stride, points, desc, counts, nullptr, 0, 0, 0);
 }
 
 int surfhip_detect(surfhip_detector* d, const uint8_t* image, int pitch, surfhip_point* points,

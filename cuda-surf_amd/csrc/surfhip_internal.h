@@ -126,9 +126,11 @@ hipError_t launch_sort(const surfhip_point* cand, const uint32_t* keys, uint64_t
 hipError_t set_max_lds(const void* fn, int bytes);
 // queue: kDescQueueBytes of device scratch (the per-XCD work counters of
 // k_describe_ur, 8 x kDescQ of them 256 B apart, zeroed by the launch)
+// beside: another stream's kernels (the next batch's integral) run beside
+// it, so the persistent grid leaves each CU a workgroup slot
 hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
                            const int* counts, const int* offsets, const int* order, int nframes, float* desc,
-                           int* queue, hipStream_t s);
+                           int* queue, hipStream_t s, bool beside = false);
 // Doubled-image input (surfhip_double.hip): frames (W x H) -> D ((2W-2) x
 // (2H-2) u8, row pitch dpitch, a multiple of 4).
 hipError_t launch_double(const uint8_t* frames, int pitch, long long fstride, int nframes, int W, int H,

@@ -439,8 +439,10 @@ __global__ __launch_bounds__(256) void k_ii_fill_w(const uint8_t* __restrict__ f
                 const uint32_t base = carry + wave_excl_scan(tot, wt);
                 carry += wt;
                 acc[t][0] += base; acc[t][1] += base + e1; acc[t][2] += base + e2; acc[t][3] += base + e3;
-                // pad columns (> W) stay zero: the flat reads of getTrace can land on them
-                if (x < ip) {
+                // pad columns (> W) stay zero (set once at detector creation and
+                // never written: 6 % of the 1080p row): the flat reads of
+                // getTrace can land on them
+                if (x <= W) {
                     const uint4 o4 = make_uint4(x <= W ? acc[t][0] : 0u, x + 1 <= W ? acc[t][1] : 0u,
                                                 x + 2 <= W ? acc[t][2] : 0u, x + 3 <= W ? acc[t][3] : 0u);
                     // nontemporal: the 2.3-GB batch integral streams past the
@@ -2883,15 +2885,33 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
     }
 }
 
+#include "surfhip_desc_u2.inc"
+
 hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
                            const int* counts, const int* offsets, const int* order, int nframes, float* desc,
-                           int* queue, hipStream_t s)
+                           int* queue, hipStream_t s, bool beside)
 {
     if (P.nfeat > 512) return hipErrorInvalidValue;
-    const int grid = 2048;
+    // the describe kernels are persistent (per-XCD keypoint queues): 2,048
+    // workgroups fill every CU; with another stream's kernels beside them
+    // (SURFHIP_DESC_BESIDE workgroups per CU, default 3) a slot stays free
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        hipDeviceProp_t pr;
+        cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&pr, dev) == hipSuccess) ? pr.multiProcessorCount
+                                                                                                   : 256;
+    }
+    static const int per_cu = getenv("SURFHIP_DESC_BESIDE") ? atoi(getenv("SURFHIP_DESC_BESIDE")) : 3;
+    const int grid = (beside && per_cu > 0) ? ((per_cu * cus + 7) & ~7) : 2048;
     hipError_t e = hipMemsetAsync(queue, 0, kDescQueueBytes, s);
     if (e != hipSuccess) return e;
-    if (P.upright && P.wsz == 4) {
+    static const bool old_ur = getenv("SURFHIP_DESC_UR") != nullptr;   // round 3's k_describe_ur (A/B)
+    if (P.upright && P.wsz == 4 && !old_ur) {
+        if (P.extend)
+            k_describe_u2<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc, queue);
+        else k_describe_u2<false><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc, queue);
+    } else if (P.upright && P.wsz == 4) {
         if (P.extend)
             k_describe_ur<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc, queue);
         else k_describe_ur<false><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc, queue);

@@ -139,6 +139,19 @@ int surfhip_detect_batch(surfhip_detector* det, const uint8_t* d_frames, int nfr
                          int pitch, size_t frame_stride, surfhip_point* d_points,
                          float* d_desc, int* d_counts);
 
+/* detect_batch with the next batch's integral image computed on the
+ * detector's side stream beside this batch's describe stage (software
+ * pipelining across batches).  The next call that passes the same
+ * next_frames (pointer, count, pitch, stride) as its `d_frames` uses the
+ * prefetched integral instead of computing it.  next_frames must hold their
+ * data when this call is made (in the detector stream's order) and stay
+ * unchanged until that next call; NULL = detect_batch.  Doubled detectors
+ * compute every integral in line. */
+int surfhip_detect_batch_next(surfhip_detector* det, const uint8_t* d_frames, int nframes,
+                              int pitch, size_t frame_stride, surfhip_point* d_points,
+                              float* d_desc, int* d_counts, const uint8_t* d_next_frames,
+                              int next_nframes, int next_pitch, size_t next_frame_stride);
+
 /* Surfor::detectAndCompute (surf.cpp:205-355) for one frame, synchronous.
  * Writes min(found, max_pts) SurfPoints to d_points, returns the count in
  * *num_pts; when desc != 0 allocates *d_desc_out = num_pts*nfeatures floats

@@ -582,3 +582,53 @@ def test_detector_geometry_pinned_to_reference_alloc_memory(surf, orc, w, h, mas
     assert giw == tuple(iwhp)
     for o in range(noct):
         assert gsw[o] == tuple(sw[3 * o:3 * o + 3]) and gos[o] == osz[o], o
+
+
+def test_detect_batch_next_equals_detect_batch(surf):
+    """surfhip_detect_batch_next (the next batch's integral computed beside
+    this batch's describe): over a sequence of batches -- the prefetch used
+    (same next frames), not used (another batch comes instead), a ragged
+    batch and a plain detect_batch in between -- every batch's keypoints and
+    descriptors are byte-identical to a detect_batch of the same frames."""
+    w, h, n = 640, 480, 12
+    frames = [surf.synth_frames(n, w, h, first=k * 100) for k in range(3)]
+    pitch = frames[0].shape[2]
+    stride = h * pitch
+    param = surf.make_param(4, 4.0, upright=True)
+    max_pts = 4096
+    bufs = []
+    for fr in frames:
+        b = surf.DeviceBuffer(fr.nbytes)
+        b.upload(fr)
+        bufs.append(b)
+    pb = surf.DeviceBuffer(48 * n * max_pts)
+    db = surf.DeviceBuffer(4 * n * max_pts * 64)
+    cb = surf.DeviceBuffer(4 * n)
+
+    def result(det_call, nf):
+        det_call()
+        surf.synchronize()
+        c = cb.download(np.int32, nf)
+        p = pb.download(surf.POINT_DTYPE, nf * max_pts).reshape(nf, max_pts)
+        d = db.download(np.float32, nf * max_pts * 64).reshape(nf, max_pts, 64)
+        return [(p[f, :c[f]].tobytes(), d[f, :c[f]].tobytes()) for f in range(nf)]
+
+    ref = surf.Detector(param, w, h, max_batch=n, max_pts=max_pts)
+    want = {}
+    for k in range(3):
+        for nf in (n, 7):
+            want[(k, nf)] = result(lambda: ref.detect_batch(bufs[k].ptr, nf, pitch, stride, pb.ptr, db.ptr, cb.ptr),
+                                   nf)
+    ref.close()
+    det = surf.Detector(param, w, h, max_batch=n, max_pts=max_pts)
+    # (batch, nframes, next batch or None, next nframes)
+    seq = [(0, n, 1, n), (1, n, 2, n), (0, n, 0, 7), (0, 7, 2, n), (2, n, None, 0), (1, n, 1, n), (1, n, 0, n),
+           (0, n, None, 0)]
+    for k, nf, nx, nnf in seq:
+        if nx is None:
+            got = result(lambda: det.detect_batch(bufs[k].ptr, nf, pitch, stride, pb.ptr, db.ptr, cb.ptr), nf)
+        else:
+            got = result(lambda: det.detect_batch_next(bufs[k].ptr, nf, pitch, stride, pb.ptr, db.ptr, cb.ptr,
+                                                       bufs[nx].ptr, nnf, pitch, stride), nf)
+        assert got == want[(k, nf)], (k, nf, nx, nnf)
+    det.close()

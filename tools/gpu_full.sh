@@ -1,0 +1,21 @@
+#!/bin/bash
+# Full GPU check: every -m gpu test, then the default bench line and a
+# kernel trace of the bench.  Each GPU step has its own time limit; the
+# script stops at the first failure.
+#   bash tools/gpu_full.sh <tag> [pytest -k expr]
+set -u
+TAG=$1; KEXPR=${2:-}
+cd /tmp && export TMPDIR=/tmp
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+O=gpurun_out
+K=(); [ -n "$KEXPR" ] && K=(-k "$KEXPR")
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread "${K[@]}" \
+    > $O/${TAG}_pytest.log 2>&1 || { tail -60 $O/${TAG}_pytest.log; exit 1; }
+tail -3 $O/${TAG}_pytest.log
+timeout -k 10 300 python3 bench.py --steps 20 --no-cpu > $O/${TAG}_bench.json 2> $O/${TAG}_bench.err || { tail -20 $O/${TAG}_bench.err; exit 1; }
+cat $O/${TAG}_bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -f csv -d $O/prof_${TAG}_kt -o run -- \
+    python3 bench.py --steps 5 --warmup 1 --no-cpu > $O/prof_${TAG}_kt.json 2> $O/prof_${TAG}_kt.err || exit 1
+f=$(ls $O/prof_${TAG}_kt/*/run_kernel_trace.csv $O/prof_${TAG}_kt/run_kernel_trace.csv 2>/dev/null | head -1); python3 tools/kstats.py $f | head -30
+echo FULL_DONE
