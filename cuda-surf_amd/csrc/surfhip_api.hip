@@ -82,6 +82,7 @@ struct surfhip_detector {
     int nitems = 0;                     // scan items per frame
     int* offsets = nullptr;
     int* order = nullptr;               // per frame: keypoint indices in row order (describe schedule)
+    float4* work = nullptr;             // the describe schedule flattened: {x, y, scale, f * max_pts + kp}
     int* status = nullptr;
     // single-frame API slots
     surfhip_point* pts1 = nullptr;
@@ -411,7 +412,7 @@ static void free_all(surfhip_detector* d)
 {
     void* ptrs[] = {d->d_oct, d->iib[0], d->iib[1], d->resp, d->colsum, d->cand, d->keys, d->gscratch, d->cand_count,
                     d->scan_key, d->scan_src, d->scan_cube, d->item_count, d->item_off,
-                    d->offsets, d->order, d->status, d->pts1, d->desc1, d->count1, d->dbl};
+                    d->offsets, d->order, d->work, d->status, d->pts1, d->desc1, d->count1, d->dbl};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (int i = 0; i < SURFHIP_NSTAGE; i++)
@@ -492,6 +493,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     ALLOC(d->item_off, (2 * B * (size_t)d->nitems + 64) * sizeof(int));
     ALLOC(d->offsets, (B + 1) * sizeof(int));
     ALLOC(d->order, B * (size_t)max_pts * sizeof(int));
+    ALLOC(d->work, B * (size_t)max_pts * sizeof(float4));
     ALLOC(d->status, 256 + kDescQueueBytes);    // [0]: flags; from [64]: describe work queues
     ALLOC(d->pts1, (size_t)max_pts * sizeof(surfhip_point));
     ALLOC(d->desc1, (size_t)max_pts * d->param.nfeatures * sizeof(float));
@@ -669,6 +671,33 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
         if (th) HIPCHK(hipEventRecord(d->hev[d->hev_n++][1], s));
         HIPCHK(hipStreamWaitEvent(s, d->join, 0));
     }
+    // The next batch's integral (into the other buffer) on the side stream,
+    // ordered after everything on s so far, so that buffer's last readers
+    // (the previous batch's fit and describe) are done.  Default: forked
+    // after this batch's Hessian, beside its NMS scan, fit and sort (the
+    // Hessian and describe then run alone); SURFHIP_PREFETCH=describe forks
+    // it after the sort instead, beside describe.
+    auto prefetch_next = [&]() -> hipError_t {
+        const int nx = d->icur ^ 1;
+        hipError_t e = hipEventRecord(d->fork2, s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(d->side, d->fork2, 0);
+        if (e == hipSuccess)
+            e = launch_integral(next_frames, next_pitch, (long long)next_stride, next_nframes, d->P, d->colsum,
+                                d->iib[nx], d->side);
+        if (e != hipSuccess) return e;
+        d->pref_valid = true;
+        d->ipref = nx;
+        d->pref_frames = next_frames;
+        d->pref_n = next_nframes;
+        d->pref_pitch = next_pitch;
+        d->pref_stride = next_stride;
+        return hipSuccess;
+    };
+    static const bool pref_nms = [] {
+        const char* e = getenv("SURFHIP_PREFETCH");
+        return !(e && !strcmp(e, "describe"));
+    }();
+    if (pipe && pref_nms) HIPCHK(prefetch_next());
     HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->scan_key, d->scan_src, d->scan_cube,
                       d->item_count,
                       d->item_off, d->cand, d->keys, d->cand_count, d->cap, s));
@@ -676,26 +705,10 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
     HIPCHK(launch_sort(d->cand, d->keys, d->gscratch, d->cand_count, d->item_off, d->plan.nms_start[kMaxOct] * 4,
                        d->cap, nframes, points, d->max_pts, counts, d->offsets, d->order, d->status, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[4], s));
-    if (pipe) {
-        // the next batch's integral, on the side stream beside this batch's
-        // describe (latency-bound gathers: HBM and issue slots to spare);
-        // ordered after everything on s so far, so the other buffer's last
-        // readers (the previous batch's fit and describe) are done
-        const int nx = d->icur ^ 1;
-        HIPCHK(hipEventRecord(d->fork2, s));
-        HIPCHK(hipStreamWaitEvent(d->side, d->fork2, 0));
-        HIPCHK(launch_integral(next_frames, next_pitch, (long long)next_stride, next_nframes, d->P, d->colsum,
-                               d->iib[nx], d->side));
-        d->pref_valid = true;
-        d->ipref = nx;
-        d->pref_frames = next_frames;
-        d->pref_n = next_nframes;
-        d->pref_pitch = next_pitch;
-        d->pref_stride = next_stride;
-    }
+    if (pipe && !pref_nms) HIPCHK(prefetch_next());
     if (desc)
-        HIPCHK(launch_describe(d->ii, d->P, points, d->max_pts, counts, d->offsets, d->order, nframes, desc,
-                               d->status + 64, s, pipe));
+        HIPCHK(launch_describe(d->ii, d->P, points, d->max_pts, counts, d->offsets, d->order, d->work, nframes, desc,
+                               d->status + 64, s, pipe && !pref_nms));
     if (prof) HIPCHK(hipEventRecord(d->ev[5], s));
     d->last_nframes = nframes;
     d->last_frames = frames;

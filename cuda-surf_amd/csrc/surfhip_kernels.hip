@@ -607,7 +607,8 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
     // (value 10 B + G: barrier interval B steps, G consumer waves)
     const char* pe = getenv("SURFHIP_P0");
     plan.p0 = (plan.q0 && !plan.q01) ? (pe ? atoi(pe) : 93) : 0;
-    if (plan.p0 != 0 && plan.p0 != 95 && plan.p0 != 93 && plan.p0 != 92 && plan.p0 != 91 && plan.p0 != 32)
+    if (plan.p0 != 0 && plan.p0 != 95 && plan.p0 != 94 && plan.p0 != 93 && plan.p0 != 92 && plan.p0 != 91 &&
+        plan.p0 != 32)
         plan.p0 = 93;
     for (int o = 0; o < kMaxOct; o++) {
         plan.hess_start[o] = hb;
@@ -735,7 +736,7 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
     else if (pb == BB && pg == GG) k_hess_p0<BB, GG, 1><<<gp, 64 * (1 + GG), 0, s>>>(frames, pitch, fstride, resp, P, \
                                                                                     h_oct[0], plan.q0_strips, nframes);
             if (false) {}
-            P0_CASE(9, 5) P0_CASE(9, 3) P0_CASE(9, 2) P0_CASE(9, 1) P0_CASE(3, 2)
+            P0_CASE(9, 5) P0_CASE(9, 4) P0_CASE(9, 3) P0_CASE(9, 2) P0_CASE(9, 1) P0_CASE(3, 2)
 #undef P0_CASE
             else if (plan.q0)
                 k_hess_q0<4, 1, 2><<<dim3(nb0), q0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
@@ -1950,6 +1951,14 @@ struct KpQueue {
         if (lane == 0) g = atomicAdd(ctr, 1);
         return gbeg + kDescQ * __builtin_amdgcn_readfirstlane(g) + qi;
     }
+    // grab() in two halves: issue the atomic, use its result later
+    __device__ int issue(int lane)
+    {
+        int g = 0;
+        if (lane == 0) g = atomicAdd(ctr, 1);
+        return g;
+    }
+    __device__ int finish(int g) { return gbeg + kDescQ * __builtin_amdgcn_readfirstlane(g) + qi; }
 };
 
 template <bool UPRIGHT, int MAXF>
@@ -2887,9 +2896,25 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
 
 #include "surfhip_desc_u2.inc"
 
+// The describe schedule flattened for k_describe_u2: entry offsets[f] + i =
+// keypoint order[f][i]'s {x, y, scale, f * max_pts + kp}, so the describe
+// loop reaches a keypoint in one load after its queue atomic (order[] and
+// pts[] were two dependent loads, and the frame a search over offsets[]).
+__global__ __launch_bounds__(256) void k_worklist(const surfhip_point* __restrict__ pts, int max_pts,
+                                                  const int* __restrict__ counts, const int* __restrict__ offsets,
+                                                  const int* __restrict__ order, float4* __restrict__ work)
+{
+    const int f = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= counts[f]) return;
+    const int idx = f * max_pts + order[(size_t)f * max_pts + i];
+    const surfhip_point p = pts[idx];
+    work[offsets[f] + i] = make_float4(p.x, p.y, p.scale, __int_as_float(idx));
+}
+
 hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
-                           const int* counts, const int* offsets, const int* order, int nframes, float* desc,
-                           int* queue, hipStream_t s, bool beside)
+                           const int* counts, const int* offsets, const int* order, float4* work, int nframes,
+                           float* desc, int* queue, hipStream_t s, bool beside)
 {
     if (P.nfeat > 512) return hipErrorInvalidValue;
     // the describe kernels are persistent (per-XCD keypoint queues): 2,048
@@ -2908,9 +2933,9 @@ hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_poin
     if (e != hipSuccess) return e;
     static const bool old_ur = getenv("SURFHIP_DESC_UR") != nullptr;   // round 3's k_describe_ur (A/B)
     if (P.upright && P.wsz == 4 && !old_ur) {
-        if (P.extend)
-            k_describe_u2<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc, queue);
-        else k_describe_u2<false><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc, queue);
+        k_worklist<<<dim3((max_pts + 255) / 256, nframes), 256, 0, s>>>(pts, max_pts, counts, offsets, order, work);
+        if (P.extend) k_describe_u2<true><<<grid, 256, 0, s>>>(ii, P, work, max_pts, offsets, nframes, desc, queue);
+        else k_describe_u2<false><<<grid, 256, 0, s>>>(ii, P, work, max_pts, offsets, nframes, desc, queue);
     } else if (P.upright && P.wsz == 4) {
         if (P.extend)
             k_describe_ur<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc, queue);
