@@ -2934,8 +2934,10 @@ hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_poin
     static const bool old_ur = getenv("SURFHIP_DESC_UR") != nullptr;   // round 3's k_describe_ur (A/B)
     if (P.upright && P.wsz == 4 && !old_ur) {
         k_worklist<<<dim3((max_pts + 255) / 256, nframes), 256, 0, s>>>(pts, max_pts, counts, offsets, order, work);
-        if (P.extend) k_describe_u2<true><<<grid, 256, 0, s>>>(ii, P, work, max_pts, offsets, nframes, desc, queue);
-        else k_describe_u2<false><<<grid, 256, 0, s>>>(ii, P, work, max_pts, offsets, nframes, desc, queue);
+        // (diagnostic: SURFHIP_U2_LDSPAD bytes of unused dynamic LDS per workgroup)
+        static const int pad = getenv("SURFHIP_U2_LDSPAD") ? atoi(getenv("SURFHIP_U2_LDSPAD")) : 0;
+        if (P.extend) k_describe_u2<true><<<grid, 256, pad, s>>>(ii, P, work, max_pts, offsets, nframes, desc, queue);
+        else k_describe_u2<false><<<grid, 256, pad, s>>>(ii, P, work, max_pts, offsets, nframes, desc, queue);
     } else if (P.upright && P.wsz == 4) {
         if (P.extend)
             k_describe_ur<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc, queue);

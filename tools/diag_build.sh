@@ -5,7 +5,7 @@
 #   bash tools/diag_build.sh NAME:FLAG[,FLAG] ...     e.g. nored:SURF_DIAG_NORED
 set -eu
 cd "$(dirname "$0")/../cuda-surf_amd"
-H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -I../include -Icsrc"
+H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -I../include -Icsrc -mllvm -amdgpu-atomic-optimizer-strategy=None"
 make -s build/surfhip_api.o build/surfhip_match.o build/surfhip_double.o
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
