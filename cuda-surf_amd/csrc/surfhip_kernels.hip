@@ -2931,8 +2931,10 @@ hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_poin
     const int grid = (beside && per_cu > 0) ? ((per_cu * cus + 7) & ~7) : 2048;
     hipError_t e = hipMemsetAsync(queue, 0, kDescQueueBytes, s);
     if (e != hipSuccess) return e;
-    static const bool old_ur = getenv("SURFHIP_DESC_UR") != nullptr;   // round 3's k_describe_ur (A/B)
-    if (P.upright && P.wsz == 4 && !old_ur) {
+    // k_describe_u2 (LDS-DMA ring) behind SURFHIP_DESC_U2=1 until its ring fix
+    // has run the determinism check on hardware; k_describe_ur otherwise
+    static const bool use_u2 = getenv("SURFHIP_DESC_U2") != nullptr && getenv("SURFHIP_DESC_UR") == nullptr;
+    if (P.upright && P.wsz == 4 && use_u2) {
         k_worklist<<<dim3((max_pts + 255) / 256, nframes), 256, 0, s>>>(pts, max_pts, counts, offsets, order, work);
         // (diagnostic: SURFHIP_U2_LDSPAD bytes of unused dynamic LDS per workgroup)
         static const int pad = getenv("SURFHIP_U2_LDSPAD") ? atoi(getenv("SURFHIP_U2_LDSPAD")) : 0;
