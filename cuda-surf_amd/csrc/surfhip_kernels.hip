@@ -2931,9 +2931,9 @@ hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_poin
     const int grid = (beside && per_cu > 0) ? ((per_cu * cus + 7) & ~7) : 2048;
     hipError_t e = hipMemsetAsync(queue, 0, kDescQueueBytes, s);
     if (e != hipSuccess) return e;
-    // k_describe_u2 (LDS-DMA ring) behind SURFHIP_DESC_U2=1 until its ring fix
-    // has run the determinism check on hardware; k_describe_ur otherwise
-    static const bool use_u2 = getenv("SURFHIP_DESC_U2") != nullptr && getenv("SURFHIP_DESC_UR") == nullptr;
+    // k_describe_u2 (LDS-DMA ring); SURFHIP_DESC_UR=1: round 3's
+    // k_describe_ur (read per launch, so a process can A/B both kernels)
+    const bool use_u2 = getenv("SURFHIP_DESC_UR") == nullptr;
     if (P.upright && P.wsz == 4 && use_u2) {
         k_worklist<<<dim3((max_pts + 255) / 256, nframes), 256, 0, s>>>(pts, max_pts, counts, offsets, order, work);
         // (diagnostic: SURFHIP_U2_LDSPAD bytes of unused dynamic LDS per workgroup)

@@ -69,6 +69,24 @@ def test_config3_batch256_vs_single_frame(surf, monkeypatch, config3):
     det.close()
 
 
+def test_config3_describe_u2_deterministic(surf, monkeypatch, config3):
+    """k_describe_u2 (LDS-DMA ring, the default) on the 256-frame batch: a
+    second run bit-identical to the first (its ring once raced: a slot
+    refilled while its reads were pending gave a few run-dependent
+    descriptors per batch), and every frame within the descriptor tolerance
+    of round 3's k_describe_ur (SURFHIP_DESC_UR=1; same keypoints, the two
+    sum in different orders)."""
+    frames, res = config3
+    param = surf.make_param(4, 4.0, upright=True)
+    again = gpu_run(surf, param, frames, W3, H3, max_pts=8192)
+    monkeypatch.setenv("SURFHIP_DESC_UR", "1")
+    ur = gpu_run(surf, param, frames, W3, H3, max_pts=8192)
+    for f in range(frames.shape[0]):
+        assert again["counts"][f] == res["counts"][f] == ur["counts"][f], f
+        assert again["desc"][f].tobytes() == res["desc"][f].tobytes(), f
+        assert desc_l2(ur["desc"][f], res["desc"][f]).max() <= DESC_TOL, f
+
+
 def test_config5_4k_rotated_extended(surf, orc):
     """Config #5 layout: 3840x2160, 5 octaves, upright=false, 128-D, as an
     8-frame batch (XCD mapping, 4K integral near the int32 limit)."""
