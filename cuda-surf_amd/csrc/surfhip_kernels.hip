@@ -2119,8 +2119,11 @@ struct RotScratch {
     };
 };
 
+#ifndef SURF_ROT_WPE
+#define SURF_ROT_WPE 3              // 3 waves per SIMD: <= 168 VGPRs (the 128-D form took 185: 2 waves)
+#endif
 template <int NB>
-__global__ __launch_bounds__(256) void k_describe_rot(const int32_t* __restrict__ ii, FrameParams P,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SURF_ROT_WPE))) void k_describe_rot(const int32_t* __restrict__ ii, FrameParams P,
                                                       surfhip_point* __restrict__ pts, int max_pts,
                                                       const int* __restrict__ offsets, const int* __restrict__ order,
                                                       int nframes, float* __restrict__ desc, int* __restrict__ queue)
