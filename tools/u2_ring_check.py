@@ -38,7 +38,10 @@ def check(x, y, sc, R=6, verbose=True):
     t0, nv = (int(vm[0]), len(vm)) if len(vm) else (0, 0)
     hmode = hs - 2 * step
     share = hmode in (0, -1)
-    dual = side <= 32
+    cs_ = (ix + (-2 - iradius) * step) & ~3
+    W4_ = (ix + (side + 1 - iradius) * step + 2 - cs_ + 3) >> 2
+    wide64 = W4_ > 32
+    dual = side <= 32 and not (wide64 and W4_ <= 64)
     j = lanes & 31 if dual else lanes
     h = lanes >> 5 if dual else np.zeros(64, int)
     sj = j - iradius
@@ -49,11 +52,11 @@ def check(x, y, sc, R=6, verbose=True):
     G = 2 if dual else 1
     cs = (ix + (-2 - iradius) * step) & ~3
     W4 = (ix + (side + 1 - iradius) * step + 2 - cs + 3) >> 2
-    seg = share and step <= 3 and W4 <= 32
+    seg = share and W4 <= 64 and (wide64 or step <= 3)
     info = dict(step=step, hs=hs, side=side, dual=dual, W4=W4, seg=seg, t0=t0, nv=nv)
     if not seg:
         return info, []
-    RSW = 64 if W4 <= 16 else 128
+    RSW = 64 if W4 <= 16 else (128 if W4 <= 32 else 256)
     cpr = RSW // 4
     nd = (2 * G * cpr + 63) // 64
     ip4 = IP * 4
