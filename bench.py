@@ -563,7 +563,9 @@ def run_rank(args):
                                           round(traffic / (hess_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)),
                          "algorithmic_bytes_per_launch": hb, "launch_ms": round(hess_ms, 4),
                          "launch_ms_source": ("in-step: HIP events around the Hessian launches of each timed "
-                                              f"step ({len(hess_instep)} steps), integral beside them"
+                                              f"step ({len(hess_instep)} steps), "
+                                              + ("the batch's own integral beside them" if args.no_pipeline else
+                                                 "the next batch's integral beside the NMS stage instead")
                                               if hess_instep else "serial"),
                          "launch_ms_serial": round(hess_serial_ms, 4)},
             "gen_s": round(gen_s, 2),
