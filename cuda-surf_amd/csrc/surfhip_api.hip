@@ -467,7 +467,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
         delete d;
         return rc;
     }
-    d->nbands = (d->H + kBandRows - 1) / kBandRows;
+    d->nbands = (d->H + big_band_rows() - 1) / big_band_rows();
     d->CW = (d->W + 1 <= 2048) ? 2048 : (d->W + 1 <= 4096 ? 4096 : 8192);
     const size_t B = (size_t)max_batch;
 #define ALLOC(ptr, bytes)                                    \

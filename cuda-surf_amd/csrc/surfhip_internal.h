@@ -10,6 +10,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <string>
 
@@ -26,10 +27,21 @@ constexpr int kDescQueueBytes = 8 * kDescQ * 64 * 4;
 constexpr int kBandRows = 32;       // integral-image band height
 constexpr int kBandRowsSmall = 8;   // ... for batches of <= kSmallBatch frames
 constexpr int kSmallBatch = 8;
+// band height for batches > kSmallBatch: kBandRows, or SURFHIP_II_BAND (8..64)
+inline int big_band_rows()
+{
+    static const int v = [] {
+        const char* e = getenv("SURFHIP_II_BAND");
+        const int b = e ? atoi(e) : kBandRows;
+        return (b >= 8 && b <= 64) ? b : kBandRows;
+    }();
+    return v;
+}
 // colsum entries (per column) the integral of a batch of up to max_batch frames needs
 inline long long integral_bands(int H, int max_batch)
 {
-    const long long big = (long long)max_batch * ((H + kBandRows - 1) / kBandRows);
+    const int bb = big_band_rows();
+    const long long big = (long long)max_batch * ((H + bb - 1) / bb);
     const long long small = (long long)(max_batch < kSmallBatch ? max_batch : kSmallBatch) *
                             ((H + kBandRowsSmall - 1) / kBandRowsSmall);
     return big > small ? big : small;

@@ -460,7 +460,7 @@ hipError_t launch_integral(const uint8_t* frames, int pitch, long long fstride, 
 {
     // small batches: 8-row bands (4x the band waves of the fill pass, which
     // is one wave per band) -- colsum is sized for both (integral_bands())
-    const int br = nframes <= kSmallBatch ? kBandRowsSmall : kBandRows;
+    const int br = nframes <= kSmallBatch ? kBandRowsSmall : big_band_rows();
     const int nbands = (P.H + br - 1) / br;
     const int W = P.W;
     dim3 grid(nbands, nframes);
