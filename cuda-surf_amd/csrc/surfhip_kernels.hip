@@ -2907,12 +2907,14 @@ __global__ __launch_bounds__(256) void k_worklist(const surfhip_point* __restric
                                                   const int* __restrict__ counts, const int* __restrict__ offsets,
                                                   const int* __restrict__ order, float4* __restrict__ work)
 {
-    const int f = blockIdx.y;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= counts[f]) return;
-    const int idx = f * max_pts + order[(size_t)f * max_pts + i];
-    const surfhip_point p = pts[idx];
-    work[offsets[f] + i] = make_float4(p.x, p.y, p.scale, __int_as_float(idx));
+    // a frame's entries over gridDim.x workgroups, strided (most of a
+    // max_pts-sized grid would find nothing to do)
+    const int f = blockIdx.y, n = counts[f], o = offsets[f];
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const int idx = f * max_pts + order[(size_t)f * max_pts + i];
+        const surfhip_point p = pts[idx];
+        work[o + i] = make_float4(p.x, p.y, p.scale, __int_as_float(idx));
+    }
 }
 
 hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
@@ -2938,7 +2940,8 @@ hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_poin
     // k_describe_ur (read per launch, so a process can A/B both kernels)
     const bool use_u2 = getenv("SURFHIP_DESC_UR") == nullptr;
     if (P.upright && P.wsz == 4 && use_u2) {
-        k_worklist<<<dim3((max_pts + 255) / 256, nframes), 256, 0, s>>>(pts, max_pts, counts, offsets, order, work);
+        k_worklist<<<dim3(std::min(8, (max_pts + 255) / 256), nframes), 256, 0, s>>>(pts, max_pts, counts, offsets,
+                                                                                      order, work);
         // (diagnostic: SURFHIP_U2_LDSPAD bytes of unused dynamic LDS per workgroup)
         static const int pad = getenv("SURFHIP_U2_LDSPAD") ? atoi(getenv("SURFHIP_U2_LDSPAD")) : 0;
         if (P.extend) k_describe_u2<true><<<grid, 256, pad, s>>>(ii, P, work, max_pts, offsets, nframes, desc, queue);
