@@ -1493,6 +1493,94 @@ __device__ void bitonic_sort_lds(uint64_t* s, int n)
     __syncthreads();
 }
 
+// The value of lane (lane ^ J) (J = 1 .. 32) of a 64-bit element, by DPP /
+// permlane swaps (no LDS round trip).
+template <int J>
+__device__ __forceinline__ uint32_t xor_lane32(uint32_t v, int lane)
+{
+    if constexpr (J == 1) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+    } else if constexpr (J == 2) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+    } else if constexpr (J == 4 || J == 8) {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x100 + J, 0xf, 0xf, false);   // lane + J
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 + J, 0xf, 0xf, false);   // lane - J
+        return (lane & J) ? dn : up;
+    } else {
+        auto r = J == 16 ? __builtin_amdgcn_permlane16_swap(v, v, false, false)
+                         : __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (lane & J) ? r[0] : r[1];
+    }
+}
+template <int J>
+__device__ __forceinline__ uint64_t xor_lane64(uint64_t v, int lane)
+{
+    return ((uint64_t)xor_lane32<J>((uint32_t)(v >> 32), lane) << 32) | xor_lane32<J>((uint32_t)v, lane);
+}
+// One compare-exchange pass (k, J <= 32) of a 128-element block held two per
+// lane (positions lane and lane + 64 of the block starting at `base`).
+template <int J>
+__device__ __forceinline__ void bitonic_reg_pass(uint64_t& e0, uint64_t& e1, int base, int k, int lane)
+{
+    const uint64_t p0 = xor_lane64<J>(e0, lane), p1 = xor_lane64<J>(e1, lane);
+    const bool lower = (lane & J) == 0;
+    const bool up0 = ((base + lane) & k) == 0, up1 = ((base + lane + 64) & k) == 0;
+    e0 = (lower == up0) ? (e0 < p0 ? e0 : p0) : (e0 < p0 ? p0 : e0);
+    e1 = (lower == up1) ? (e1 < p1 ? e1 : p1) : (e1 < p1 ? p1 : e1);
+}
+__device__ __forceinline__ void bitonic_reg_tail(uint64_t& e0, uint64_t& e1, int base, int k, int jmax, int lane)
+{
+    // passes J = jmax .. 1 (jmax <= 32)
+    if (jmax >= 32) bitonic_reg_pass<32>(e0, e1, base, k, lane);
+    if (jmax >= 16) bitonic_reg_pass<16>(e0, e1, base, k, lane);
+    if (jmax >= 8) bitonic_reg_pass<8>(e0, e1, base, k, lane);
+    if (jmax >= 4) bitonic_reg_pass<4>(e0, e1, base, k, lane);
+    if (jmax >= 2) bitonic_reg_pass<2>(e0, e1, base, k, lane);
+    bitonic_reg_pass<1>(e0, e1, base, k, lane);
+}
+
+// The same network with every pass of distance <= 64 in registers: a wave
+// holds a 128-element block two per lane and runs those passes with DPP /
+// permlane swaps; only the passes of distance >= 128 go through LDS (with a
+// workgroup barrier each).  n >= 128, blockDim.x == 1024.
+__device__ void bitonic_sort_lds_reg(uint64_t* s, int n)
+{
+    const int lane = (int)lane_id(), wv = (int)(threadIdx.x >> 6);
+    const int nblk = n >> 7;
+    // k = 2 .. 64: within blocks only
+    for (int b = wv; b < nblk; b += 16) {
+        const int base = b << 7;
+        uint64_t e0 = s[base + lane], e1 = s[base + lane + 64];
+        for (int k = 2; k <= 64; k <<= 1) bitonic_reg_tail(e0, e1, base, k, k >> 1, lane);
+        s[base + lane] = e0;
+        s[base + lane + 64] = e1;
+    }
+    __syncthreads();
+    const int npairs = n >> 1;
+    for (int k = 128; k <= n; k <<= 1) {
+        for (int j = k >> 1; j >= 128; j >>= 1) {
+            for (int p = threadIdx.x; p < npairs; p += 1024) {
+                const int i = 2 * p - (p & (j - 1));
+                const uint64_t a = s[i], b = s[i + j];
+                const bool up = (i & k) == 0;
+                if ((a > b) == up) { s[i] = b; s[i + j] = a; }
+            }
+            __syncthreads();
+        }
+        for (int b = wv; b < nblk; b += 16) {
+            const int base = b << 7;
+            uint64_t e0 = s[base + lane], e1 = s[base + lane + 64];
+            // distance 64: the lane's own two elements
+            const bool up = (base & k) == 0;
+            if ((e0 > e1) == up) { const uint64_t t = e0; e0 = e1; e1 = t; }
+            bitonic_reg_tail(e0, e1, base, k, 32, lane);
+            s[base + lane] = e0;
+            s[base + lane + 64] = e1;
+        }
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(1024) void k_sort(const surfhip_point* __restrict__ cand,
                                                const uint32_t* __restrict__ keys,
                                                uint64_t* __restrict__ gscratch, const int* __restrict__ cand_count,
@@ -1519,7 +1607,12 @@ __global__ __launch_bounds__(1024) void k_sort(const surfhip_point* __restrict__
     }
     if (mine) atomicAdd(&nvalid, mine);
     __syncthreads();
+#ifdef SURF_SORT_LDSONLY
     if (in_lds && blockDim.x == 1024) bitonic_sort_lds(s, n);
+#else
+    if (in_lds && blockDim.x == 1024 && n >= 128) bitonic_sort_lds_reg(s, n);
+    else if (in_lds && blockDim.x == 1024) bitonic_sort_lds(s, n);
+#endif
     else bitonic_sort(s, n);
     const int valid = nvalid;
     // accepted candidates beyond the cap were dropped: report it
