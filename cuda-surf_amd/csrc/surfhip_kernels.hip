@@ -1309,20 +1309,25 @@ __global__ __launch_bounds__(256) void k_scan_local(const int* __restrict__ in, 
 
 __global__ __launch_bounds__(1024) void k_scan_top(int* __restrict__ bsum, int nb, int* __restrict__ out, int n)
 {
-    __shared__ int part[1024];
+    __shared__ int part[16];
     const int per = (nb + 1023) / 1024;
     const int b = threadIdx.x * per;
     int sum = 0;
     for (int i = 0; i < per; i++) if (b + i < nb) sum += bsum[b + i];
-    part[threadIdx.x] = sum;
+    // exclusive scan of the 1,024 partial sums: DPP wave scans and the 16
+    // wave totals (was one thread walking all 1,024)
+    const uint32_t inc = wave_incl_scan((uint32_t)sum);
+    const int wv = (int)(threadIdx.x >> 6);
+    if (lane_id() == 63) part[wv] = (int)inc;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        int run = 0;
-        for (int t = 0; t < 1024; t++) { const int v = part[t]; part[t] = run; run += v; }
-        out[n] = run;
+    uint32_t wbase = 0u, total = 0u;
+    for (int t = 0; t < 16; t++) {
+        const uint32_t v = (uint32_t)part[t];
+        wbase += t < wv ? v : 0u;
+        total += v;
     }
-    __syncthreads();
-    int run = part[threadIdx.x];
+    if (threadIdx.x == 0) out[n] = (int)total;
+    int run = (int)(wbase + inc) - sum;
     for (int i = 0; i < per; i++)
         if (b + i < nb) { const int v = bsum[b + i]; bsum[b + i] = run; run += v; }
 }
@@ -1727,20 +1732,26 @@ __global__ __launch_bounds__(256) void k_sort_rank(const surfhip_point* __restri
 
 __global__ __launch_bounds__(1024) void k_offsets(const int* __restrict__ counts, int nframes, int* __restrict__ offsets)
 {
-    __shared__ int part[1024];
+    __shared__ int part[16];
     const int per = (nframes + 1023) / 1024;
     const int b = threadIdx.x * per;
     int sum = 0;
     for (int i = 0; i < per; i++) if (b + i < nframes) sum += counts[b + i];
-    part[threadIdx.x] = sum;
+    // exclusive scan of the 1,024 partial sums: DPP wave scans and the 16
+    // wave totals (was one thread walking all 1,024: ~10 us, on config #2's
+    // single-frame path too)
+    const uint32_t inc = wave_incl_scan((uint32_t)sum);
+    const int wv = (int)(threadIdx.x >> 6);
+    if (lane_id() == 63) part[wv] = (int)inc;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        int run = 0;
-        for (int t = 0; t < 1024; t++) { const int v = part[t]; part[t] = run; run += v; }
-        offsets[nframes] = run;
+    uint32_t wbase = 0u, total = 0u;
+    for (int t = 0; t < 16; t++) {
+        const uint32_t v = (uint32_t)part[t];
+        wbase += t < wv ? v : 0u;
+        total += v;
     }
-    __syncthreads();
-    int run = part[threadIdx.x];
+    if (threadIdx.x == 0) offsets[nframes] = (int)total;
+    int run = (int)(wbase + inc) - sum;
     for (int i = 0; i < per; i++)
         if (b + i < nframes) { offsets[b + i] = run; run += counts[b + i]; }
 }
