@@ -105,6 +105,7 @@ _sigs = {
     "surfhip_make_param": (_i, [C.POINTER(SurfParam), _i, C.c_float, _i, _i, _i, _i, _i, _i]),
     "surfhip_detect_batch": (_i, [_vp, _vp, _i, _i, _sz, _vp, _vp, _vp]),
     "surfhip_detect_batch_next": (_i, [_vp, _vp, _i, _i, _sz, _vp, _vp, _vp, _vp, _i, _i, _sz]),
+    "surfhip_detector_drain": (_i, [_vp]),
     "surfhip_detect": (_i, [_vp, _vp, _i, _vp, _i, C.POINTER(_i), C.POINTER(_vp), _i]),
     "surfhip_detector_candidates": (_i, [_vp, C.POINTER(_i), _i]),
     "surfhip_detector_status": (_i, [_vp, C.POINTER(_i)]),
@@ -279,7 +280,8 @@ class Detector:
         check(_lib.surfhip_detector_time_hessian(self.h, int(on)), "time_hessian")
 
     def hessian_times(self) -> list:
-        """Milliseconds of each recorded batch's Hessian launches (and reset)."""
+        """Milliseconds of each recorded batch's whole Hessian stage, from its
+        fork to the end of its last kernel on either stream (and reset)."""
         ms = (C.c_float * 64)()
         n = _i(0)
         check(_lib.surfhip_detector_hessian_times(self.h, ms, 64, C.byref(n)), "hessian_times")
@@ -303,6 +305,11 @@ class Detector:
         check(_lib.surfhip_detect_batch_next(self.h, frames_ptr, nframes, pitch, stride, points_ptr, desc_ptr,
                                              counts_ptr, next_ptr, next_nframes, next_pitch, next_stride),
               "detect_batch_next")
+
+    def drain(self) -> None:
+        """Order the side stream's pending prefetch before the detector
+        stream's later work (surfhip_detector_drain)."""
+        check(_lib.surfhip_detector_drain(self.h), "drain")
 
     def run_integral(self, frames_ptr, nframes, pitch, stride) -> None:
         check(_lib.surfhip_run_integral(self.h, frames_ptr, nframes, pitch, stride), "run_integral")

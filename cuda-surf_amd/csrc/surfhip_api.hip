@@ -46,6 +46,7 @@ static inline int align_up(int a, int b) { return (a % b != 0) ? (a - a % b + b)
 
 struct surfhip_detector {
     int dev = 0;
+    int cus = 256;                      // compute units of dev (the describe kernels' persistent grid)
     hipStream_t stream = nullptr;
     surfhip_param param{};
     FrameParams P{};
@@ -94,7 +95,11 @@ struct surfhip_detector {
     hipEvent_t fork = nullptr, join = nullptr;
     float stage_ms[SURFHIP_NSTAGE]{};
     bool time_hess = false;             // in-step Hessian event pairs (surfhip_detector_time_hessian)
-    hipEvent_t hev[SURFHIP_MAX_HESS_EV][2]{};
+    // per timed batch: [0] on the detector stream before the Hessian's fork,
+    // [1] on it after the u8 kernels, [2] on the side stream after the
+    // integral-image kernels (only when the plan has some: hev_side)
+    hipEvent_t hev[SURFHIP_MAX_HESS_EV][3]{};
+    bool hev_side[SURFHIP_MAX_HESS_EV]{};
     int hev_n = 0;
     int last_nframes = 0;
     const uint8_t* last_frames = nullptr;   // u8 source of the last integral (surfhip_run_hessian)
@@ -418,7 +423,7 @@ static void free_all(surfhip_detector* d)
     for (int i = 0; i < SURFHIP_NSTAGE; i++)
         if (d->ev[i]) (void)hipEventDestroy(d->ev[i]);
     for (int i = 0; i < SURFHIP_MAX_HESS_EV; i++)
-        for (int j = 0; j < 2; j++)
+        for (int j = 0; j < 3; j++)
             if (d->hev[i][j]) (void)hipEventDestroy(d->hev[i][j]);
     if (d->fork) (void)hipEventDestroy(d->fork);
     if (d->fork2) (void)hipEventDestroy(d->fork2);
@@ -456,6 +461,11 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     d->cap = c2;
     d->stream = (hipStream_t)stream;
     hipError_t e = hipGetDevice(&d->dev);
+    if (e == hipSuccess) {
+        hipDeviceProp_t pr;
+        e = hipGetDeviceProperties(&pr, d->dev);
+        if (e == hipSuccess) d->cus = pr.multiProcessorCount;
+    }
     rc = (e == hipSuccess) ? derive(d) : SURFHIP_ERR_HIP;
     // the NMS survivor records pack the sample row / column into 14 bits and
     // the block row of the canonical key into 13 (k_nms_scan): octave 0 is
@@ -644,7 +654,11 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
     HIPCHK(hipMemsetAsync(d->status, 0, sizeof(int), s));       // per-batch truncation flag
     HIPCHK(hipMemsetAsync(d->item_count, 0, sizeof(int) * (size_t)nframes * d->nitems, s));
     if (prof) {
-        // serial, so that the stage events bracket each stage alone
+        // serial, so that the stage events bracket each stage alone; a
+        // prefetch left on the side stream by an earlier pipelined call may
+        // still be using the colsum scratch the integral below reuses
+        HIPCHK(hipEventRecord(d->join, d->side));
+        HIPCHK(hipStreamWaitEvent(s, d->join, 0));
         HIPCHK(hipEventRecord(d->ev[0], s));
         HIPCHK(source_frames(d, frames, pitch, stride, nframes, s));
         HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, s));
@@ -656,19 +670,30 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
         // the u8 Hessian kernels need no integral image: they run on s; the
         // integral (unless prefetched) and the integral-image Hessian kernels
         // run on the side stream beside them; s waits for both before NMS
+        // In-step Hessian timing brackets the WHOLE stage: from the fork (on
+        // s) to the end of the u8 kernels on s and of the integral-image
+        // kernels on the side stream, whichever is later
+        // (surfhip_detector_hessian_times).  Without a prefetched integral
+        // the side stream's part starts after the integral, which the
+        // bracket then includes.
         HIPCHK(source_frames(d, frames, pitch, stride, nframes, s));
+        const bool th = d->time_hess && d->hev_n < SURFHIP_MAX_HESS_EV;
+        const bool side_hess = d->plan.hess_start[kMaxOct] > 0;
+        if (th) HIPCHK(hipEventRecord(d->hev[d->hev_n][0], s));
         HIPCHK(hipEventRecord(d->fork, s));
         HIPCHK(hipStreamWaitEvent(d->side, d->fork, 0));
         if (!have)
             HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, d->side));
         HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
                               d->plan, d->side, 2));
+        if (th && side_hess) HIPCHK(hipEventRecord(d->hev[d->hev_n][2], d->side));
         HIPCHK(hipEventRecord(d->join, d->side));
-        const bool th = d->time_hess && d->hev_n < SURFHIP_MAX_HESS_EV;
-        if (th) HIPCHK(hipEventRecord(d->hev[d->hev_n][0], s));
         HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
                               d->plan, s, 1));
-        if (th) HIPCHK(hipEventRecord(d->hev[d->hev_n++][1], s));
+        if (th) {
+            HIPCHK(hipEventRecord(d->hev[d->hev_n][1], s));
+            d->hev_side[d->hev_n++] = side_hess;
+        }
         HIPCHK(hipStreamWaitEvent(s, d->join, 0));
     }
     // The next batch's integral (into the other buffer) on the side stream,
@@ -708,12 +733,23 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
     if (pipe && !pref_nms) HIPCHK(prefetch_next());
     if (desc)
         HIPCHK(launch_describe(d->ii, d->P, points, d->max_pts, counts, d->offsets, d->order, d->work, nframes, desc,
-                               d->status + 64, s, pipe && !pref_nms));
+                               d->status + 64, s, pipe && !pref_nms, d->cus));
     if (prof) HIPCHK(hipEventRecord(d->ev[5], s));
     d->last_nframes = nframes;
     d->last_frames = frames;
     d->last_pitch = pitch;
     d->last_fstride = (long long)stride;
+    return SURFHIP_OK;
+}
+
+int surfhip_detector_drain(surfhip_detector* d)
+{
+    if (!d) return SURFHIP_ERR_INVALID;
+    // everything queued on the side stream so far (a prefetch of the next
+    // batch's integral, which reads next_frames) is ordered before the
+    // detector stream's later work
+    HIPCHK(hipEventRecord(d->join, d->side));
+    HIPCHK(hipStreamWaitEvent(d->stream, d->join, 0));
     return SURFHIP_OK;
 }
 
@@ -799,7 +835,7 @@ int surfhip_detector_time_hessian(surfhip_detector* d, int on)
     if (!d) return SURFHIP_ERR_INVALID;
     if (on) {
         for (int i = 0; i < SURFHIP_MAX_HESS_EV; i++)
-            for (int j = 0; j < 2; j++)
+            for (int j = 0; j < 3; j++)
                 if (!d->hev[i][j]) HIPCHK(hipEventCreate(&d->hev[i][j]));
     }
     d->time_hess = on != 0;
@@ -814,6 +850,12 @@ int surfhip_detector_hessian_times(surfhip_detector* d, float* ms, int max, int*
     for (int i = 0; i < k; i++) {
         HIPCHK(hipEventSynchronize(d->hev[i][1]));
         HIPCHK(hipEventElapsedTime(&ms[i], d->hev[i][0], d->hev[i][1]));
+        if (d->hev_side[i]) {
+            float t2 = 0.f;
+            HIPCHK(hipEventSynchronize(d->hev[i][2]));
+            HIPCHK(hipEventElapsedTime(&t2, d->hev[i][0], d->hev[i][2]));
+            ms[i] = std::max(ms[i], t2);
+        }
     }
     *n = k;
     d->hev_n = 0;

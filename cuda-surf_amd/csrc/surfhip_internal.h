@@ -141,9 +141,10 @@ hipError_t set_max_lds(const void* fn, int bytes);
 // beside: another stream's kernels (the next batch's integral) run beside
 // it, so the persistent grid leaves each CU a workgroup slot
 // work: max_batch * max_pts float4 of scratch (k_describe_u2's flattened schedule)
+// cus: compute units of the detector's device (sizes the persistent grid)
 hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
                            const int* counts, const int* offsets, const int* order, float4* work, int nframes,
-                           float* desc, int* queue, hipStream_t s, bool beside = false);
+                           float* desc, int* queue, hipStream_t s, bool beside, int cus);
 // Doubled-image input (surfhip_double.hip): frames (W x H) -> D ((2W-2) x
 // (2H-2) u8, row pitch dpitch, a multiple of 4).
 hipError_t launch_double(const uint8_t* frames, int pitch, long long fstride, int nframes, int W, int H,

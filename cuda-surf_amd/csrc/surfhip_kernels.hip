@@ -3023,26 +3023,21 @@ __global__ __launch_bounds__(256) void k_worklist(const surfhip_point* __restric
 
 hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
                            const int* counts, const int* offsets, const int* order, float4* work, int nframes,
-                           float* desc, int* queue, hipStream_t s, bool beside)
+                           float* desc, int* queue, hipStream_t s, bool beside, int cus)
 {
     if (P.nfeat > 512) return hipErrorInvalidValue;
     // the describe kernels are persistent (per-XCD keypoint queues): 2,048
     // workgroups fill every CU; with another stream's kernels beside them
     // (SURFHIP_DESC_BESIDE workgroups per CU, default 3) a slot stays free
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        hipDeviceProp_t pr;
-        cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&pr, dev) == hipSuccess) ? pr.multiProcessorCount
-                                                                                                   : 256;
-    }
+    if (cus <= 0) cus = 256;
     static const int per_cu = getenv("SURFHIP_DESC_BESIDE") ? atoi(getenv("SURFHIP_DESC_BESIDE")) : 3;
     const int grid = (beside && per_cu > 0) ? ((per_cu * cus + 7) & ~7) : 2048;
     hipError_t e = hipMemsetAsync(queue, 0, kDescQueueBytes, s);
     if (e != hipSuccess) return e;
     // k_describe_u2 (LDS-DMA ring); SURFHIP_DESC_UR=1: round 3's
     // k_describe_ur (read per launch, so a process can A/B both kernels)
-    const bool use_u2 = getenv("SURFHIP_DESC_UR") == nullptr;
+    const char* ur = getenv("SURFHIP_DESC_UR");
+    const bool use_u2 = !(ur && atoi(ur) != 0);
     if (P.upright && P.wsz == 4 && use_u2) {
         k_worklist<<<dim3(std::min(8, (max_pts + 255) / 256), nframes), 256, 0, s>>>(pts, max_pts, counts, offsets,
                                                                                       order, work);

@@ -145,12 +145,18 @@ int surfhip_detect_batch(surfhip_detector* det, const uint8_t* d_frames, int nfr
  * next_frames (pointer, count, pitch, stride) as its `d_frames` uses the
  * prefetched integral instead of computing it.  next_frames must hold their
  * data when this call is made (in the detector stream's order) and stay
- * unchanged until that next call; NULL = detect_batch.  Doubled detectors
- * compute every integral in line. */
+ * unchanged until that next call, or until surfhip_detector_drain; NULL =
+ * detect_batch.  Doubled detectors compute every integral in line. */
 int surfhip_detect_batch_next(surfhip_detector* det, const uint8_t* d_frames, int nframes,
                               int pitch, size_t frame_stride, surfhip_point* d_points,
                               float* d_desc, int* d_counts, const uint8_t* d_next_frames,
                               int next_nframes, int next_pitch, size_t next_frame_stride);
+
+/* Orders the detector's side-stream work (a pending prefetch of the next
+ * batch's integral, which reads next_frames) before anything later on the
+ * detector's stream: after drain, synchronising that stream means
+ * next_frames are no longer read.  The prefetch stays valid. */
+int surfhip_detector_drain(surfhip_detector* det);
 
 /* Surfor::detectAndCompute (surf.cpp:205-355) for one frame, synchronous.
  * Writes min(found, max_pts) SurfPoints to d_points, returns the count in

@@ -1,8 +1,10 @@
-"""Multi-process (gloo, world_size 2, CPU) test of the frame sharding and the
+"""Multi-process (gloo, world_size 2 and 8, CPU) test of the frame sharding and the
 single all-gather of compacted result slabs.  Each rank runs
 the CPU oracle on its contiguous shard of a synthetic batch, packs the
 results in the libsurfhip slab format, and all-gathers; every rank must then
-hold exactly the concatenation of the per-frame single-process results."""
+hold exactly the concatenation of the per-frame single-process results.
+World 8 with 11 frames rehearses config #4's layout (one rank per GPU of a
+node) with a batch that 8 does not divide: shards of 1 and 2 frames."""
 from __future__ import annotations
 
 import os
@@ -41,6 +43,7 @@ def _worker(rank, world, port, n_frames, w, h, q):
         counts.append(len(pt))
         pts.append(pt)
         descs.append(d)
+    assert count >= 1
     slab = surf.build_slab(np.array(counts, np.int32), np.concatenate(pts), np.concatenate(descs))
     cap = surf.dist.agree_slab_size(dist, torch, len(slab), "cpu")
     buf = torch.zeros(cap, dtype=torch.uint8)
@@ -55,7 +58,7 @@ def _worker(rank, world, port, n_frames, w, h, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_frames", [(2, 4), (2, 3)])
+@pytest.mark.parametrize("world,n_frames", [(2, 4), (2, 3), (8, 11)])
 def test_shard_and_allgather_gloo(world, n_frames):
     torch = pytest.importorskip("torch")
     import torch.multiprocessing as mp
@@ -68,7 +71,8 @@ def test_shard_and_allgather_gloo(world, n_frames):
     procs = [ctx.Process(target=_worker, args=(r, world, port, n_frames, w, h, q)) for r in range(world)]
     for pr in procs:
         pr.start()
-    results = [q.get(timeout=180) for _ in range(world)]
+    results = [q.get(timeout=300) for _ in range(world)]
+    assert sorted(r[0] for r in results) == list(range(world))
     for pr in procs:
         pr.join(timeout=60)
         assert pr.exitcode == 0

@@ -632,3 +632,52 @@ def test_detect_batch_next_equals_detect_batch(surf):
                                                        bufs[nx].ptr, nnf, pitch, stride), nf)
         assert got == want[(k, nf)], (k, nf, nx, nnf)
     det.close()
+
+
+def test_profiled_call_after_pipelined_call(surf):
+    """A pipelined call leaves the next batch's integral running on the side
+    stream (sharing the colsum scratch); a stage-profiled call queued right
+    after it (no host sync in between) must wait for it, and
+    surfhip_detector_drain keeps the prefetch valid: every result equals a
+    plain detect_batch of the same frames."""
+    w, h, n = 1920, 1080, 16
+    frames = [surf.synth_frames(n, w, h, first=k * 50) for k in range(3)]
+    pitch = frames[0].shape[2]
+    stride = h * pitch
+    param = surf.make_param(4, 4.0, upright=True)
+    max_pts = 8192
+    bufs = []
+    for fr in frames:
+        b = surf.DeviceBuffer(fr.nbytes)
+        b.upload(fr)
+        bufs.append(b)
+    pb = surf.DeviceBuffer(48 * n * max_pts)
+    db = surf.DeviceBuffer(4 * n * max_pts * 64)
+    cb = surf.DeviceBuffer(4 * n)
+
+    def fetch():
+        surf.synchronize()
+        c = cb.download(np.int32, n)
+        p = pb.download(surf.POINT_DTYPE, n * max_pts).reshape(n, max_pts)
+        d = db.download(np.float32, n * max_pts * 64).reshape(n, max_pts, 64)
+        return [(p[f, :c[f]].tobytes(), d[f, :c[f]].tobytes()) for f in range(n)]
+
+    ref = surf.Detector(param, w, h, max_batch=n, max_pts=max_pts)
+    want = []
+    for k in range(3):
+        ref.detect_batch(bufs[k].ptr, n, pitch, stride, pb.ptr, db.ptr, cb.ptr)
+        want.append(fetch())
+    ref.close()
+    det = surf.Detector(param, w, h, max_batch=n, max_pts=max_pts)
+    det.detect_batch_next(bufs[0].ptr, n, pitch, stride, pb.ptr, db.ptr, cb.ptr, bufs[1].ptr, n, pitch, stride)
+    det.set_profiling(True)
+    det.detect_batch(bufs[2].ptr, n, pitch, stride, pb.ptr, db.ptr, cb.ptr)
+    assert fetch() == want[2]
+    assert det.stage_times()["total"] > 0
+    det.set_profiling(False)
+    det.detect_batch_next(bufs[0].ptr, n, pitch, stride, pb.ptr, db.ptr, cb.ptr, bufs[1].ptr, n, pitch, stride)
+    assert fetch() == want[0]
+    det.drain()
+    det.detect_batch_next(bufs[1].ptr, n, pitch, stride, pb.ptr, db.ptr, cb.ptr, None, 0, 0, 0)
+    assert fetch() == want[1]
+    det.close()
