@@ -68,3 +68,30 @@ def test_cpu_share_reports_host():
     assert 1 <= share <= host["host_cpus"]
     assert share <= host["affinity_cpus"]
     assert host["cpu_model"]
+
+
+def test_committed_hessian_profiles_consistent():
+    """profiles/hessian_profile.json (bench.py's frac_profile / bound source,
+    written by tools/hessian_profile.py) holds one entry per single-GPU config
+    whose stage time is the sum of its kernels' rocprof averages, a bound
+    the rule allows, and utilisations that justify it; bench.py finds the
+    entry for its config only when the kernel names match."""
+    import json
+    b = _bench()
+    d = json.load(open(os.path.join(REPO, "profiles", "hessian_profile.json")))
+    assert {"256x1920x1080x4u", "1x1920x1080x4u", "64x3840x2160x5rx"} <= set(d)
+    for key, e in d.items():
+        assert abs(e["stage_ms"] - sum(e["kernels_avg_ns"].values()) * 1e-6) < 1e-9, key
+        ev = e["bound_evidence"]
+        units = {"hbm": ev.get("hbm_util", 0), "valu-issue": ev.get("valu_util", 0), "lds": ev.get("lds_util", 0)}
+        top = max(units, key=units.get)
+        assert e["bound"] == (top if units[top] >= 0.6 else "latency"), key
+        assert os.path.exists(os.path.join(REPO, "profiles", f"{e['tag']}_kernel_stats.csv")), key
+
+    class A:
+        width, height, octaves, upright, extend, batch = 1920, 1080, 4, 1, 0, 256
+    e = b.hessian_profile(A, "k_hess_p0 (octave 0) + k_hess_w (octaves 1-3)")
+    assert e is not None and set(e["kernels_avg_ns"]) == {"k_hess_p0", "k_hess_w"}
+    assert b.hessian_profile(A, "k_hess_q0 (octave 0) + k_hess_w (octaves 1-3)") is None
+    A.batch = 1
+    assert b.hessian_profile(A, "k_hessian (octaves 0-3)")["kernels_avg_ns"].keys() == {"k_hessian"}
