@@ -667,9 +667,6 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
                               d->plan, s));
         HIPCHK(hipEventRecord(d->ev[2], s));
     } else {
-        // the u8 Hessian kernels need no integral image: they run on s; the
-        // integral (unless prefetched) and the integral-image Hessian kernels
-        // run on the side stream beside them; s waits for both before NMS
         // In-step Hessian timing brackets the WHOLE stage: from the fork (on
         // s) to the end of the u8 kernels on s and of the integral-image
         // kernels on the side stream, whichever is later
@@ -678,23 +675,47 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
         // bracket then includes.
         HIPCHK(source_frames(d, frames, pitch, stride, nframes, s));
         const bool th = d->time_hess && d->hev_n < SURFHIP_MAX_HESS_EV;
-        const bool side_hess = d->plan.hess_start[kMaxOct] > 0;
         if (th) HIPCHK(hipEventRecord(d->hev[d->hev_n][0], s));
-        HIPCHK(hipEventRecord(d->fork, s));
-        HIPCHK(hipStreamWaitEvent(d->side, d->fork, 0));
-        if (!have)
-            HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, d->side));
-        HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
-                              d->plan, d->side, 2));
-        if (th && side_hess) HIPCHK(hipEventRecord(d->hev[d->hev_n][2], d->side));
-        HIPCHK(hipEventRecord(d->join, d->side));
-        HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
-                              d->plan, s, 1));
-        if (th) {
-            HIPCHK(hipEventRecord(d->hev[d->hev_n][1], s));
-            d->hev_side[d->hev_n++] = side_hess;
+        if (!plan_reads_frames(d->plan)) {
+            // Every Hessian kernel reads the integral image (the gather plan
+            // of batches <= kGatherBatch, config #2): nothing would run beside
+            // them, so they stay on the detector stream -- the fork / join
+            // round trip through the side stream cost a one-frame step ~30 us
+            // of idle GPU in a kernel trace (profiles/r05ac2_*).  The side
+            // stream's last work (a prefetch into d->ii, or one using the
+            // colsum scratch) is ordered first; it finished long ago.
+            HIPCHK(hipEventRecord(d->join, d->side));
+            HIPCHK(hipStreamWaitEvent(s, d->join, 0));
+            if (!have)
+                HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, s));
+            HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct,
+                                  d->oct, d->plan, s, 2));
+            if (th) {
+                HIPCHK(hipEventRecord(d->hev[d->hev_n][1], s));
+                d->hev_side[d->hev_n++] = false;
+            }
+        } else {
+            // the u8 Hessian kernels need no integral image: they run on s;
+            // the integral (unless prefetched) and the integral-image Hessian
+            // kernels run on the side stream beside them; s waits for both
+            // before NMS
+            const bool side_hess = d->plan.hess_start[kMaxOct] > 0;
+            HIPCHK(hipEventRecord(d->fork, s));
+            HIPCHK(hipStreamWaitEvent(d->side, d->fork, 0));
+            if (!have)
+                HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, d->side));
+            HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct,
+                                  d->oct, d->plan, d->side, 2));
+            if (th && side_hess) HIPCHK(hipEventRecord(d->hev[d->hev_n][2], d->side));
+            HIPCHK(hipEventRecord(d->join, d->side));
+            HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct,
+                                  d->oct, d->plan, s, 1));
+            if (th) {
+                HIPCHK(hipEventRecord(d->hev[d->hev_n][1], s));
+                d->hev_side[d->hev_n++] = side_hess;
+            }
+            HIPCHK(hipStreamWaitEvent(s, d->join, 0));
         }
-        HIPCHK(hipStreamWaitEvent(s, d->join, 0));
     }
     // The next batch's integral (into the other buffer) on the side stream,
     // ordered after everything on s so far, so that buffer's last readers

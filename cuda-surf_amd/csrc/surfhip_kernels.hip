@@ -242,14 +242,16 @@ __global__ __launch_bounds__(256) void k_ii_bandscan(uint32_t* __restrict__ cols
     if (x >= W) return;
     uint32_t* c = colsum + (size_t)f * nbands * CW + x;
     uint32_t run = 0u;
-    // 16 bands' loads in flight per chunk (one memory latency per chunk,
-    // not per band)
-    for (int b0 = 0; b0 < nbands; b0 += 16) {
-        uint32_t v[16];
+    // 48 bands' loads in flight per chunk (one memory latency per chunk, not
+    // per band: a single frame's 135 8-row bands took 9 round trips at 16,
+    // 12 us, profiles/r05ac2_kernel_stats.csv)
+    constexpr int CH = 48;
+    for (int b0 = 0; b0 < nbands; b0 += CH) {
+        uint32_t v[CH];
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = (b0 + k < nbands) ? c[(size_t)(b0 + k) * CW] : 0u;
+        for (int k = 0; k < CH; k++) v[k] = (b0 + k < nbands) ? c[(size_t)(b0 + k) * CW] : 0u;
 #pragma unroll
-        for (int k = 0; k < 16; k++)
+        for (int k = 0; k < CH; k++)
             if (b0 + k < nbands) {
                 c[(size_t)(b0 + k) * CW] = run;
                 run += v[k];
@@ -1716,11 +1718,22 @@ __global__ __launch_bounds__(256) void k_sort_rank(const surfhip_point* __restri
     if (lds) {
         const uint4* s4 = reinterpret_cast<const uint4*>(sk);
         const int n4 = cnt >> 2;
-        for (int j = 0; j < n4; j++) {
+        // 8 broadcast reads in flight per iteration: one LDS round trip per
+        // 32 keys, not per 4 (the loop was one latency per uint4: 29 us for
+        // a 1080p frame's ~3,000 candidates, profiles/r05ac2_kernel_stats.csv)
+        int j = 0;
+        for (; j + 8 <= n4; j += 8) {
+            uint4 q[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) q[u] = s4[j + u];
+#pragma unroll
+            for (int u = 0; u < 8; u++) rank += (q[u].x < ki) + (q[u].y < ki) + (q[u].z < ki) + (q[u].w < ki);
+        }
+        for (; j < n4; j++) {
             const uint4 q = s4[j];                          // broadcast read
             rank += (q.x < ki) + (q.y < ki) + (q.z < ki) + (q.w < ki);
         }
-        for (int j = n4 * 4; j < cnt; j++) rank += sk[j] < ki;
+        for (int jj = n4 * 4; jj < cnt; jj++) rank += sk[jj] < ki;
     } else {
         for (int j = 0; j < cnt; j++) rank += fk[j] < ki;
     }
