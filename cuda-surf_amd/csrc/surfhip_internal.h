@@ -107,6 +107,7 @@ struct LaunchPlan {
     int q01;                        // q0 and q1 in one launch (k_hess_q01)
     int hw_n;                       // octaves 1 .. hw_n on k_hess_w (u8, shared strip integral); 0: off
     int hw_nstrips, hw_nblk;        // its strips per frame and blocks of 4 integral rows
+    int t0, t0_nbx, t0_nby;         // octave 0 of the gather plan on k_hessian_t0 (LDS tiles): its blocks
 };
 // the plan has kernels that read the u8 frames (not only the integral image)
 inline bool plan_reads_frames(const LaunchPlan& p) { return p.q0 || p.q1 || p.hw_n > 0; }

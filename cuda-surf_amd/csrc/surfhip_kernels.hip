@@ -562,6 +562,12 @@ static bool q0_ok(const FrameParams& P, const OctaveParams& q)
     return true;
 }
 
+// k_hessian_t0 (octave 0 of the gather plan from LDS tiles): sample rows per
+// workgroup and the corners' reach it stages (16 for init mask 9: lobe 11,
+// m + x2 = 16)
+constexpr int kT0BY = 8;
+constexpr int kT0Halo = 16;
+
 // Octaves 1 .. n of the default geometry (sampling 2, init mask 9: lobes
 // 15/19/23, 31/39/47, 63/79/95) on k_hess_w; returns n (2 or 3) or 0.
 static int hw_octaves(const FrameParams& P, const OctaveParams* oct)
@@ -612,6 +618,18 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
     if (plan.p0 != 0 && plan.p0 != 95 && plan.p0 != 94 && plan.p0 != 93 && plan.p0 != 92 && plan.p0 != 91 &&
         plan.p0 != 32)
         plan.p0 = 93;
+    // the gather plan's octave 0 from LDS tiles (k_hessian_t0) when its
+    // corners reach at most kT0Halo integral samples from the sample and the
+    // sampling step is 2 (the default geometry); SURFHIP_HESS_T0=0 disables
+    {
+        const char* te = getenv("SURFHIP_HESS_T0");
+        const OctaveParams& q = oct[0];
+        int reach = 0;
+        for (int i = 0; i < q.nscale; i++) reach = std::max(reach, std::max(q.mask[i] + q.x2[i], q.x4[i]));
+        plan.t0 = gather && P.noct > 0 && q.delta == 2 && reach <= kT0Halo && !(te && atoi(te) == 0);
+        plan.t0_nbx = (q.sw + 63) / 64;
+        plan.t0_nby = (q.sh + kT0BY - 1) / kT0BY;
+    }
     for (int o = 0; o < kMaxOct; o++) {
         plan.hess_start[o] = hb;
         plan.nms_start[o] = nb;
@@ -619,7 +637,7 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
             const OctaveParams& q = oct[o];
             plan.hess_nbx[o] = (q.sw + 63) / 64;
             const bool on_u8 = (o == 0 && plan.q0) || (o == 1 && plan.q1) || (o >= 1 && o <= plan.hw_n);
-            if (!on_u8) hb += plan.hess_nbx[o] * ((q.sh + 3) / 4);
+            if (!on_u8 && !(o == 0 && plan.t0)) hb += plan.hess_nbx[o] * ((q.sh + 3) / 4);
             plan.nms_nbx[o] = (q.nms_gx + 63) / 64;
             plan.nms_nby[o] = (q.nms_gy + kScanRows - 1) / kScanRows;
             nb += ((P.max_scale - 1) / 2) * plan.nms_nbx[o] * plan.nms_nby[o];   // levels k = 1, 3, .. < max_scale - 1
@@ -648,6 +666,7 @@ std::string hessian_plan_text(const LaunchPlan& plan, const FrameParams& P)
         else if (plan.q0) add("k_hess_q0", 0, 0);
         if (plan.q1) add("k_hess_q1", 1, 1);
     }
+    if (plan.t0) add("k_hessian_t0", 0, 0);
     if (plan.hw_n > 0) add("k_hess_w", 1, plan.hw_n);
     if (plan.hess_start[kMaxOct] > 0) {
         int lo = -1, hi = -1;
@@ -716,6 +735,60 @@ __global__ __launch_bounds__(256) void k_hessian(const int32_t* __restrict__ ii,
     }
 }
 
+// Octave 0 of the gather plan (few frames, config #2) from LDS tiles: a
+// workgroup loads the integral-image tile under its 64 x kT0BY samples (the
+// samples' span plus every corner's reach, kT0Halo on each side) with
+// coalesced row loads, then each thread computes its samples' scales with
+// hessian_at reading the tile -- the 32 corners of a response are LDS reads
+// instead of global gathers (k_hessian: 32 dependent-latency gathers per
+// response, 55 us for one 1080p frame's four octaves, 80 % of the responses
+// in octave 0).  Same integer box sums and float ops as k_hessian, so the
+// planes are bit-identical.
+template <int HALO>
+__global__ __launch_bounds__(256) void k_hessian_t0(const int32_t* __restrict__ ii, float* __restrict__ resp,
+                                                    FrameParams P, OctaveParams q, int nbx, int nby, int nframes)
+{
+    constexpr int TW = 2 * 63 + 2 * HALO + 2;           // tile columns: integral x in [2 ix0 - HALO, ..]
+    constexpr int TH = 2 * (kT0BY - 1) + 2 * HALO + 2;  // tile rows
+    __shared__ uint32_t T[TH * TW];
+    int f, lb;
+    if (!xcd_frame_block(nbx * nby, nframes, f, lb)) return;
+    const int by = lb / nbx, bx = lb - by * nbx;
+    const int ix0 = bx * 64, iy0 = by * kT0BY;
+    const int tx0 = 2 * ix0 - HALO, ty0 = 2 * iy0 - HALO;
+    const uint32_t* I = reinterpret_cast<const uint32_t*>(ii) + (size_t)f * P.ii_stride;
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    // rows by wave, columns by lane (coalesced); coordinates outside the
+    // image are clamped -- only samples outside the borders, which are not
+    // computed, would read them
+    for (int r = wv; r < TH; r += 4) {
+        const int gy = min(max(ty0 + r, 0), P.iH - 1);
+        const uint32_t* row = I + (size_t)gy * P.ip;
+#pragma unroll
+        for (int c0 = 0; c0 < TW; c0 += 64) {
+            const int c = c0 + lane;
+            if (c < TW) T[r * TW + c] = row[min(max(tx0 + c, 0), P.ip - 1)];
+        }
+    }
+    __syncthreads();
+    const int ix = ix0 + lane;
+    for (int k = wv; k < kT0BY; k += 4) {
+        const int iy = iy0 + k;
+        if (ix >= q.sw || iy >= q.sh) continue;
+        float* R = resp + (size_t)f * P.resp_stride + q.ooff + (size_t)iy * q.sp + ix;
+        const int lx = 2 * lane + HALO, ly = 2 * k + HALO;          // (x0, y0) in the tile
+#pragma unroll
+        for (int i = 0; i < kMaxScale; i++) {
+            if (i >= q.nscale) break;
+            const int b1 = q.b1[i];
+            float v = 0.f;
+            if (ix >= b1 && ix < q.sw - b1 && iy >= b1 && iy < q.sh - b1)
+                v = hessian_at(T, TW, lx, ly, q.mask[i], q.x2[i], q.x3[i], q.x4[i]) * q.norm[i];
+            R[(size_t)(q.init_scale + i) * q.osize] = v;
+        }
+    }
+}
+
 hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, const int32_t* ii, float* resp,
                           int nframes, const FrameParams& P, const OctaveParams* d_oct, const OctaveParams* h_oct,
                           const LaunchPlan& plan, hipStream_t s, int parts)
@@ -758,6 +831,9 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
                                                       plan.hw_nstrips, nframes, plan.hw_nblk);
         }
     }
+    if (plan.t0 && iip)
+        k_hessian_t0<kT0Halo><<<dim3(frame_grid(nframes) * plan.t0_nbx * plan.t0_nby), 256, 0, s>>>(
+            ii, resp, P, h_oct[0], plan.t0_nbx, plan.t0_nby, nframes);
     if (plan.hess_start[kMaxOct] > 0 && iip)
         k_hessian<<<dim3(frame_grid(nframes) * plan.hess_start[kMaxOct]), 256, 0, s>>>(ii, resp, P, d_oct, plan,
                                                                                         nframes);

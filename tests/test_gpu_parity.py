@@ -149,7 +149,8 @@ def _extreme_frame(kind, w, h, pitch):
 
 
 @pytest.mark.parametrize("kind", ["white", "noise", "vstripes", "checker", "hbands", "vbands"])
-@pytest.mark.parametrize("env", ["SURFHIP_HESS_W=1", "SURFHIP_HESS_W=0", "SURFHIP_P0=0", "SURFHIP_P0=95"])
+@pytest.mark.parametrize("env", ["SURFHIP_HESS_W=1", "SURFHIP_HESS_W=0", "SURFHIP_P0=0", "SURFHIP_P0=95",
+                                 "SURFHIP_HESS_GATHER=1"])
 def test_hessian_planes_extreme_frames(surf, orc, monkeypatch, kind, env):
     w, h = 1920, 1080
     name, _, val = env.partition("=")
@@ -166,12 +167,13 @@ def test_hessian_planes_extreme_frames(surf, orc, monkeypatch, kind, env):
 
 
 @pytest.mark.parametrize("env", ["SURFHIP_HESS_W=0", "SURFHIP_HESS_W=0,SURFHIP_Q01=0", "SURFHIP_HESS_GATHER=1",
-                                 "SURFHIP_P0=0", "SURFHIP_P0=95", "SURFHIP_P0=92", "SURFHIP_P0=91", "SURFHIP_P0=32"])
+                                 "SURFHIP_HESS_GATHER=1,SURFHIP_HESS_T0=0", "SURFHIP_P0=0", "SURFHIP_P0=95", "SURFHIP_P0=92", "SURFHIP_P0=91", "SURFHIP_P0=32"])
 @pytest.mark.parametrize("w,h,noct", [(640, 480, 4), (1920, 1080, 4), (1920, 1080, 2), (960, 540, 3)])
 def test_hessian_alternate_kernels_bit_exact(surf, orc, monkeypatch, env, w, h, noct):
     """The selectable Hessian plans give the same planes: k_hess_q1 (alone or
     merged with k_hess_q0 in k_hess_q01) + the gather kernel instead of
-    k_hess_w, the all-gather plan, octave 0 on k_hess_q0 instead of k_hess_p0
+    k_hess_w, the gather plan (octave 0 from LDS tiles, k_hessian_t0, or every
+    octave on k_hessian), octave 0 on k_hess_q0 instead of k_hess_p0
     and k_hess_p0 with 3-step barrier intervals; 2 octaves (no k_hess_w) and 3 octaves
     (k_hess_w with octaves 1-2).  The plan reads these switches when a
     detector is created."""
