@@ -83,7 +83,7 @@ struct surfhip_detector {
     int nitems = 0;                     // scan items per frame
     int* offsets = nullptr;
     int* order = nullptr;               // per frame: keypoint indices in row order (describe schedule)
-    float4* work = nullptr;             // the describe schedule flattened: {x, y, scale, f * max_pts + kp}
+    float4* work = nullptr;             // the describe schedule flattened: 2 float4 per keypoint (k_worklist)
     int* status = nullptr;
     // single-frame API slots
     surfhip_point* pts1 = nullptr;
@@ -503,7 +503,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     ALLOC(d->item_off, (2 * B * (size_t)d->nitems + 64) * sizeof(int));
     ALLOC(d->offsets, (B + 1) * sizeof(int));
     ALLOC(d->order, B * (size_t)max_pts * sizeof(int));
-    ALLOC(d->work, B * (size_t)max_pts * sizeof(float4));
+    ALLOC(d->work, B * (size_t)max_pts * 2 * sizeof(float4));
     ALLOC(d->status, 256 + kDescQueueBytes);    // [0]: flags; from [64]: describe work queues
     ALLOC(d->pts1, (size_t)max_pts * sizeof(surfhip_point));
     ALLOC(d->desc1, (size_t)max_pts * d->param.nfeatures * sizeof(float));

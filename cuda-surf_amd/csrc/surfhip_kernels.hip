@@ -1382,7 +1382,12 @@ __global__ __launch_bounds__(256) void k_scan_local(const int* __restrict__ in, 
 #pragma unroll
     for (int k = 0; k < 8; k++)
         if (b0 + k < n) out[b0 + k] = (int)v[k];
-    if (threadIdx.x == 255) bsum[blockIdx.x] = (int)(v[7] + last);
+    if (threadIdx.x == 255) {
+        // one chunk (n <= kScanChunk: a frame or two's NMS items): the total
+        // goes straight to out[n] and the other two kernels are not launched
+        if (gridDim.x == 1) out[n] = (int)(v[7] + last);
+        else bsum[blockIdx.x] = (int)(v[7] + last);
+    }
 }
 
 __global__ __launch_bounds__(1024) void k_scan_top(int* __restrict__ bsum, int nb, int* __restrict__ out, int n)
@@ -1421,6 +1426,7 @@ static void launch_excl_scan(const int* in, int n, int* out, int* bsum, hipStrea
 {
     const int nb = (n + kScanChunk - 1) / kScanChunk;
     k_scan_local<<<nb, 256, 0, s>>>(in, n, out, bsum);
+    if (nb == 1) return;
     k_scan_top<<<1, 1024, 0, s>>>(bsum, nb, out, n);
     k_scan_add<<<nb, 256, 0, s>>>(out, n, bsum);
 }
@@ -1770,10 +1776,18 @@ __global__ __launch_bounds__(256) void k_sort_rank(const surfhip_point* __restri
     const bool lds = cnt <= kRankLds;
     int mine = 0;
     if (lds) {
-        for (int i = threadIdx.x; i < cnt; i += 256) {
-            const uint32_t k = fk[i];
-            sk[i] = k;
-            mine += k != kNoKey;
+        // 8 loads in flight per thread (a loop of single loads waited a
+        // memory latency per 256 keys)
+        for (int i0 = threadIdx.x; i0 < cnt; i0 += 256 * 8) {
+            uint32_t k[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) k[u] = (i0 + 256 * u < cnt) ? fk[i0 + 256 * u] : kNoKey;
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (i0 + 256 * u < cnt) {
+                    sk[i0 + 256 * u] = k[u];
+                    mine += k[u] != kNoKey;
+                }
         }
     } else {
         for (int i = threadIdx.x; i < cnt; i += 256) mine += fk[i] != kNoKey;
@@ -3109,15 +3123,29 @@ __global__ __launch_bounds__(256) void k_describe_ur(const int32_t* __restrict__
 // pts[] were two dependent loads, and the frame a search over offsets[]).
 __global__ __launch_bounds__(256) void k_worklist(const surfhip_point* __restrict__ pts, int max_pts,
                                                   const int* __restrict__ counts, const int* __restrict__ offsets,
-                                                  const int* __restrict__ order, float4* __restrict__ work)
+                                                  const int* __restrict__ order, float4* __restrict__ work,
+                                                  FrameParams P)
 {
     // a frame's entries over gridDim.x workgroups, strided (most of a
-    // max_pts-sized grid would find nothing to do)
+    // max_pts-sized grid would find nothing to do).  Entry = two float4 of
+    // the keypoint's window geometry, the describe kernel's per-keypoint
+    // set-up moved here (surfd.cu:1581-1596, the upright branch of describe):
+    //   {dx, dy, spacing, f}  {ix, iy, step | hs << 8 | iradius << 20, f * max_pts + kp}
     const int f = blockIdx.y, n = counts[f], o = offsets[f];
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const int idx = f * max_pts + order[(size_t)f * max_pts + i];
         const surfhip_point p = pts[idx];
-        work[o + i] = make_float4(p.x, p.y, p.scale, __int_as_float(idx));
+        const DescAt at = desc_at(P.doubled, p);
+        const float scale = at.scale;
+        const int step = max(f2i_rn(scale * 0.5f), 1);
+        const int ix = f2i_rn(at.x), iy = f2i_rn(at.y);
+        const float spacing = scale * (float)P.mag;
+        const int hs = f2i_rz(scale);
+        const int iradius = f2i_rn(((spacing * (float)(P.wsz + 1)) * 0.5f) / (float)step);
+        work[2 * (size_t)(o + i)] = make_float4(at.x - (float)ix, at.y - (float)iy, spacing, __int_as_float(f));
+        work[2 * (size_t)(o + i) + 1] =
+            make_float4(__int_as_float(ix), __int_as_float(iy), __int_as_float(step | (hs << 8) | (iradius << 20)),
+                        __int_as_float(idx));
     }
 }
 
@@ -3140,7 +3168,7 @@ hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_poin
     const bool use_u2 = !(ur && atoi(ur) != 0);
     if (P.upright && P.wsz == 4 && use_u2) {
         k_worklist<<<dim3(std::min(8, (max_pts + 255) / 256), nframes), 256, 0, s>>>(pts, max_pts, counts, offsets,
-                                                                                      order, work);
+                                                                                      order, work, P);
         // (diagnostic: SURFHIP_U2_LDSPAD bytes of unused dynamic LDS per workgroup)
         static const int pad = getenv("SURFHIP_U2_LDSPAD") ? atoi(getenv("SURFHIP_U2_LDSPAD")) : 0;
         if (P.extend) k_describe_u2<true><<<grid, 256, pad, s>>>(ii, P, work, max_pts, offsets, nframes, desc, queue);
