@@ -1757,6 +1757,13 @@ __global__ __launch_bounds__(1024) void k_sort(const surfhip_point* __restrict__
 // (staged in LDS when they fit).  Processing order for describe = canonical.
 constexpr int kRankBatch = 8;
 constexpr int kRankLds = 16384;
+// Rank sort of a frame's candidates (small batches): a valid key's rank
+// among the frame's keys is its canonical position (keys are unique).  16
+// lanes share a candidate, each counting the smaller keys in every 16th slot
+// (lane-interleaved LDS reads), then a 16-lane DPP sum: 16 candidates per
+// workgroup.  (One lane per candidate walked all ~3,000 keys of a 1080p
+// frame on one wave per SIMD of a dozen CUs: 27-29 us per frame.)
+constexpr int kRankT = 16;                      // lanes per candidate
 __global__ __launch_bounds__(256) void k_sort_rank(const surfhip_point* __restrict__ cand,
                                                    const uint32_t* __restrict__ keys,
                                                    const int* __restrict__ cand_count,
@@ -1767,30 +1774,27 @@ __global__ __launch_bounds__(256) void k_sort_rank(const surfhip_point* __restri
 {
     __shared__ __attribute__((aligned(16))) uint32_t sk[kRankLds];
     __shared__ int nvalid;
+    constexpr int CPW = 256 / kRankT;           // candidates per workgroup
     const int f = blockIdx.x / wgs_per_frame, r = blockIdx.x - f * wgs_per_frame;
     const int cnt = min(soff[(f + 1) * items_per_frame] - soff[f * items_per_frame], cap);
     const uint32_t* fk = keys + (size_t)f * cap;
-    if (r > 0 && r * 256 >= cnt) return;      // nothing to rank here (workgroup 0 writes the count)
+    if (r > 0 && r * CPW >= cnt) return;        // nothing to rank here (workgroup 0 writes the count)
     if (threadIdx.x == 0) nvalid = 0;
     __syncthreads();
     const bool lds = cnt <= kRankLds;
     int mine = 0;
-    if (lds) {
-        // 8 loads in flight per thread (a loop of single loads waited a
-        // memory latency per 256 keys)
-        for (int i0 = threadIdx.x; i0 < cnt; i0 += 256 * 8) {
-            uint32_t k[8];
+    // 8 loads in flight per thread (a loop of single loads waited a memory
+    // latency per 256 keys)
+    for (int i0 = threadIdx.x; i0 < cnt; i0 += 256 * 8) {
+        uint32_t k[8];
 #pragma unroll
-            for (int u = 0; u < 8; u++) k[u] = (i0 + 256 * u < cnt) ? fk[i0 + 256 * u] : kNoKey;
+        for (int u = 0; u < 8; u++) k[u] = (i0 + 256 * u < cnt) ? fk[i0 + 256 * u] : kNoKey;
 #pragma unroll
-            for (int u = 0; u < 8; u++)
-                if (i0 + 256 * u < cnt) {
-                    sk[i0 + 256 * u] = k[u];
-                    mine += k[u] != kNoKey;
-                }
-        }
-    } else {
-        for (int i = threadIdx.x; i < cnt; i += 256) mine += fk[i] != kNoKey;
+        for (int u = 0; u < 8; u++)
+            if (i0 + 256 * u < cnt) {
+                if (lds) sk[i0 + 256 * u] = k[u];
+                mine += k[u] != kNoKey;
+            }
     }
     if (mine) atomicAdd(&nvalid, mine);
     __syncthreads();
@@ -1800,34 +1804,32 @@ __global__ __launch_bounds__(256) void k_sort_rank(const surfhip_point* __restri
         out_count[f] = keep;
         if (cand_count[f] > valid) atomicOr(status, 1);
     }
-    const int i = r * 256 + (int)threadIdx.x;
-    if (i >= cnt) return;
-    const uint32_t ki = lds ? sk[i] : fk[i];
-    if (ki == kNoKey) return;
+    const int part = (int)(threadIdx.x & (kRankT - 1));
+    const int i = r * CPW + (int)(threadIdx.x / kRankT);
+    const uint32_t ki = (i < cnt) ? (lds ? sk[i] : fk[i]) : kNoKey;
     int rank = 0;
-    if (lds) {
-        const uint4* s4 = reinterpret_cast<const uint4*>(sk);
-        const int n4 = cnt >> 2;
-        // 8 broadcast reads in flight per iteration: one LDS round trip per
-        // 32 keys, not per 4 (the loop was one latency per uint4: 29 us for
-        // a 1080p frame's ~3,000 candidates, profiles/r05ac2_kernel_stats.csv)
-        int j = 0;
-        for (; j + 8 <= n4; j += 8) {
-            uint4 q[8];
+    if (ki != kNoKey) {
+        if (lds) {
+            int j = part;
+            for (; j + 7 * kRankT < cnt; j += 8 * kRankT) {
+                uint32_t q[8];
 #pragma unroll
-            for (int u = 0; u < 8; u++) q[u] = s4[j + u];
+                for (int u = 0; u < 8; u++) q[u] = sk[j + u * kRankT];
 #pragma unroll
-            for (int u = 0; u < 8; u++) rank += (q[u].x < ki) + (q[u].y < ki) + (q[u].z < ki) + (q[u].w < ki);
+                for (int u = 0; u < 8; u++) rank += q[u] < ki;
+            }
+            for (; j < cnt; j += kRankT) rank += sk[j] < ki;
+        } else {
+            for (int j = part; j < cnt; j += kRankT) rank += fk[j] < ki;
         }
-        for (; j < n4; j++) {
-            const uint4 q = s4[j];                          // broadcast read
-            rank += (q.x < ki) + (q.y < ki) + (q.z < ki) + (q.w < ki);
-        }
-        for (int jj = n4 * 4; jj < cnt; jj++) rank += sk[jj] < ki;
-    } else {
-        for (int j = 0; j < cnt; j++) rank += fk[j] < ki;
     }
-    if (rank < keep) {
+    // the 16 partial counts of a candidate: DPP row shifts (16-lane rows)
+    rank += __builtin_amdgcn_update_dpp(0, rank, 0x111, 0xf, 0xf, false);      // row_shr:1
+    rank += __builtin_amdgcn_update_dpp(0, rank, 0x112, 0xf, 0xf, false);      // row_shr:2
+    rank += __builtin_amdgcn_update_dpp(0, rank, 0x114, 0xf, 0xf, false);      // row_shr:4
+    rank += __builtin_amdgcn_update_dpp(0, rank, 0x118, 0xf, 0xf, false);      // row_shr:8
+    // lane 15 of each row holds the row's sum
+    if (part == kRankT - 1 && ki != kNoKey && rank < keep) {
         out[(size_t)f * max_pts + rank] = cand[(size_t)f * cap + i];
         order[(size_t)f * max_pts + rank] = rank;
     }
@@ -1865,7 +1867,7 @@ hipError_t launch_sort(const surfhip_point* cand, const uint32_t* keys, uint64_t
                        hipStream_t s)
 {
     if (nframes <= kRankBatch && getenv("SURFHIP_SORT_BITONIC") == nullptr) {
-        const int per = (cap + 255) / 256;
+        const int per = (cap + 256 / kRankT - 1) / (256 / kRankT);
         k_sort_rank<<<nframes * per, 256, 0, s>>>(cand, keys, cand_count, soff, items_per_frame, cap, per, out,
                                                   max_pts, out_count, order, status);
     } else {
