@@ -236,16 +236,17 @@ __global__ __launch_bounds__(256) void k_ii_bandsum(const uint8_t* __restrict__ 
         *reinterpret_cast<uint4*>(dst + k) = make_uint4(acc[k], acc[k + 1], acc[k + 2], acc[k + 3]);
 }
 
+template <int CH>
 __global__ __launch_bounds__(256) void k_ii_bandscan(uint32_t* __restrict__ colsum, int nbands, int CW, int W)
 {
     const int x = blockIdx.x * 256 + threadIdx.x, f = blockIdx.y;
     if (x >= W) return;
     uint32_t* c = colsum + (size_t)f * nbands * CW + x;
     uint32_t run = 0u;
-    // 48 bands' loads in flight per chunk (one memory latency per chunk, not
-    // per band: a single frame's 135 8-row bands took 9 round trips at 16,
-    // 12 us, profiles/r05ac2_kernel_stats.csv)
-    constexpr int CH = 48;
+    // CH bands' loads in flight per chunk (one memory latency per chunk, not
+    // per band): 48 for the 32-row bands of a batch, 136 for the 8-row bands
+    // of a single 1080p frame (135 bands: 9 round trips at 16, 12 us,
+    // profiles/r05ac2_kernel_stats.csv)
     for (int b0 = 0; b0 < nbands; b0 += CH) {
         uint32_t v[CH];
 #pragma unroll
@@ -457,6 +458,12 @@ __global__ __launch_bounds__(256) void k_ii_fill_w(const uint8_t* __restrict__ f
     }
 }
 
+static void launch_bandscan(uint32_t* colsum, int nbands, int CW, int W, int nframes, hipStream_t s)
+{
+    if (nbands <= 48) k_ii_bandscan<48><<<dim3((W + 255) / 256, nframes), 256, 0, s>>>(colsum, nbands, CW, W);
+    else k_ii_bandscan<136><<<dim3((W + 255) / 256, nframes), 256, 0, s>>>(colsum, nbands, CW, W);
+}
+
 hipError_t launch_integral(const uint8_t* frames, int pitch, long long fstride, int nframes,
                            const FrameParams& P, uint32_t* colsum, int32_t* ii, hipStream_t s)
 {
@@ -469,13 +476,13 @@ hipError_t launch_integral(const uint8_t* frames, int pitch, long long fstride, 
     if (W + 1 <= 2048) {
         const int CW = 2048;
         k_ii_bandsum<8><<<grid, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW, br);
-        k_ii_bandscan<<<dim3((W + 255) / 256, nframes), 256, 0, s>>>(colsum, nbands, CW, W);
+        launch_bandscan(colsum, nbands, CW, W, nframes, s);
         k_ii_fill_w<8><<<(nbands * nframes + 3) / 4, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW,
                                                                     ii, P.ip, P.ii_stride, nframes, br);
     } else if (W + 1 <= 4096) {
         const int CW = 4096;
         k_ii_bandsum<16><<<grid, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW, br);
-        k_ii_bandscan<<<dim3((W + 255) / 256, nframes), 256, 0, s>>>(colsum, nbands, CW, W);
+        launch_bandscan(colsum, nbands, CW, W, nframes, s);
         k_ii_fill_w<16><<<(nbands * nframes + 3) / 4, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum,
                                                                      CW, ii, P.ip, P.ii_stride, nframes, br);
     } else if (W + 1 <= 8192) {
@@ -483,7 +490,7 @@ hipError_t launch_integral(const uint8_t* frames, int pitch, long long fstride, 
         // workgroup-scan fill (one 256-thread block per band, two barriers a row)
         const int CW = 8192;
         k_ii_bandsum<32><<<grid, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW, br);
-        k_ii_bandscan<<<dim3((W + 255) / 256, nframes), 256, 0, s>>>(colsum, nbands, CW, W);
+        launch_bandscan(colsum, nbands, CW, W, nframes, s);
         k_ii_fill<32><<<grid, 256, 0, s>>>(frames, pitch, fstride, W, P.H, nbands, colsum, CW, ii, P.ip, P.ii_stride,
                                            br);
     } else {
@@ -1518,8 +1525,11 @@ hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const F
 {
     const int per = plan.nms_start[kMaxOct];
     if (per == 0) return hipSuccess;
+    // the scan's fit records for every batch size (round 5: one 1080p frame's
+    // NMS 0.038 -> 0.034 ms with them; round 2's cross-lane variant had made
+    // single frames slower)
     static const char* ce = getenv("SURFHIP_FIT_CUBE");                  // A/B: 0 off, 1 on
-    const bool cube = ce ? atoi(ce) != 0 : nframes > kGatherBatch;
+    const bool cube = ce ? atoi(ce) != 0 : true;
     if (!cube) scan_cube = nullptr;
     auto* scan = cube ? &k_nms_scan<true> : &k_nms_scan<false>;
     scan<<<dim3(frame_grid(nframes) * per), 256, 0, s>>>(resp, P, d_oct, plan, scan_key, scan_src, scan_cube,
@@ -3166,8 +3176,12 @@ hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_poin
     if (e != hipSuccess) return e;
     // k_describe_u2 (LDS-DMA ring); SURFHIP_DESC_UR=1: round 3's
     // k_describe_ur (read per launch, so a process can A/B both kernels)
+    // (SURFHIP_DESC_UR=1 / 0 forces k_describe_ur / k_describe_u2; default:
+    // k_describe_ur for batches of <= kGatherBatch frames, where a wave gets
+    // about one keypoint and the ring's fill latency is not amortised --
+    // one 1080p frame's describe 0.032 -> 0.030 ms)
     const char* ur = getenv("SURFHIP_DESC_UR");
-    const bool use_u2 = !(ur && atoi(ur) != 0);
+    const bool use_u2 = ur ? atoi(ur) == 0 : nframes > kGatherBatch;
     if (P.upright && P.wsz == 4 && use_u2) {
         k_worklist<<<dim3(std::min(8, (max_pts + 255) / 256), nframes), 256, 0, s>>>(pts, max_pts, counts, offsets,
                                                                                       order, work, P);

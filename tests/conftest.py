@@ -21,6 +21,9 @@ import pytest
 # kernels the batched path uses (a detector with max_batch <= 8 would pick the
 # gather kernel); tests of the gather plan set SURFHIP_HESS_GATHER=1 themselves.
 os.environ.setdefault("SURFHIP_HESS_GATHER", "0")
+# ... and on k_describe_u2 (the batched default; batches <= 8 frames pick
+# k_describe_ur): tests of the small-batch default unset it themselves.
+os.environ.setdefault("SURFHIP_DESC_UR", "0")
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(REPO, "tests", "golden")

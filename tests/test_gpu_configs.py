@@ -87,6 +87,23 @@ def test_config3_describe_u2_deterministic(surf, monkeypatch, config3):
         assert desc_l2(ur["desc"][f], res["desc"][f]).max() <= DESC_TOL, f
 
 
+def test_small_batch_default_plan(surf, orc, monkeypatch):
+    """The plan a detector of <= 8 frames picks by default (config #2): the
+    gather Hessian with octave 0 from LDS tiles, fit records, k_describe_ur --
+    keypoints bit-exact and descriptors within tolerance of the oracle."""
+    monkeypatch.delenv("SURFHIP_HESS_GATHER", raising=False)
+    monkeypatch.delenv("SURFHIP_DESC_UR", raising=False)
+    monkeypatch.delenv("SURFHIP_FIT_CUBE", raising=False)
+    w, h = 1920, 1080
+    frames = surf.synth_frames(2, w, h, first=900)
+    param = surf.make_param(4, 4.0, upright=True)
+    res = gpu_run(surf, param, frames, w, h, max_pts=8192)
+    op = orc.make_param(4, 4.0, upright=True)
+    for f in range(2):
+        o_pts, o_desc, nc = orc.detect(op, frames[f], w, h, max_pts=8192)
+        compare_frame(res["pts"][f], res["desc"][f], o_pts, o_desc, True)
+
+
 def test_config5_4k_rotated_extended(surf, orc):
     """Config #5 layout: 3840x2160, 5 octaves, upright=false, 128-D, as an
     8-frame batch (XCD mapping, 4K integral near the int32 limit)."""
