@@ -461,7 +461,8 @@ __global__ __launch_bounds__(256) void k_ii_fill_w(const uint8_t* __restrict__ f
 static void launch_bandscan(uint32_t* colsum, int nbands, int CW, int W, int nframes, hipStream_t s)
 {
     if (nbands <= 48) k_ii_bandscan<48><<<dim3((W + 255) / 256, nframes), 256, 0, s>>>(colsum, nbands, CW, W);
-    else k_ii_bandscan<136><<<dim3((W + 255) / 256, nframes), 256, 0, s>>>(colsum, nbands, CW, W);
+    else if (nbands <= 136) k_ii_bandscan<136><<<dim3((W + 255) / 256, nframes), 256, 0, s>>>(colsum, nbands, CW, W);
+    else k_ii_bandscan<272><<<dim3((W + 255) / 256, nframes), 256, 0, s>>>(colsum, nbands, CW, W);
 }
 
 hipError_t launch_integral(const uint8_t* frames, int pitch, long long fstride, int nframes,
@@ -469,7 +470,7 @@ hipError_t launch_integral(const uint8_t* frames, int pitch, long long fstride, 
 {
     // small batches: 8-row bands (4x the band waves of the fill pass, which
     // is one wave per band) -- colsum is sized for both (integral_bands())
-    const int br = nframes <= kSmallBatch ? kBandRowsSmall : big_band_rows();
+    const int br = nframes <= kSmallBatch ? small_band_rows() : big_band_rows();
     const int nbands = (P.H + br - 1) / br;
     const int W = P.W;
     dim3 grid(nbands, nframes);
