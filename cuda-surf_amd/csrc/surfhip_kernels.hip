@@ -624,7 +624,7 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
     const char* pe = getenv("SURFHIP_P0");
     plan.p0 = (plan.q0 && !plan.q01) ? (pe ? atoi(pe) : 93) : 0;
     if (plan.p0 != 0 && plan.p0 != 95 && plan.p0 != 94 && plan.p0 != 93 && plan.p0 != 92 && plan.p0 != 91 &&
-        plan.p0 != 32)
+        plan.p0 != 32 && plan.p0 != 33)
         plan.p0 = 93;
     // the gather plan's octave 0 from LDS tiles (k_hessian_t0) when its
     // corners reach at most kT0Halo integral samples from the sample and the
@@ -819,7 +819,7 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
     else if (pb == BB && pg == GG) k_hess_p0<BB, GG, 1><<<gp, 64 * (1 + GG), 0, s>>>(frames, pitch, fstride, resp, P, \
                                                                                     h_oct[0], plan.q0_strips, nframes);
             if (false) {}
-            P0_CASE(9, 5) P0_CASE(9, 4) P0_CASE(9, 3) P0_CASE(9, 2) P0_CASE(9, 1) P0_CASE(3, 2)
+            P0_CASE(9, 5) P0_CASE(9, 4) P0_CASE(9, 3) P0_CASE(9, 2) P0_CASE(9, 1) P0_CASE(3, 2) P0_CASE(3, 3)
 #undef P0_CASE
             else if (plan.q0)
                 k_hess_q0<4, 1, 2><<<dim3(nb0), q0::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
