@@ -49,6 +49,17 @@ def main():
         for r in csv.DictReader(open(path)):
             rows[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
     kernels = sorted({k for k, _ in rows})
+    sq_path = os.path.join(args.src, f"prof_{t}_sq", "run_counter_collection.csv")
+    if os.path.exists(sq_path):
+        sq = collections.defaultdict(list)
+        for r in csv.DictReader(open(sq_path)):
+            sq[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+        with open(os.path.join(prof, f"{t}_sq.txt"), "w") as fh:
+            fh.write(f"# rocprofv3 --pmc SQ counters (one pass), tools/profile_round.sh {t}; "
+                     "mean per launch\n")
+            for (k, c) in sorted(x for x in sq if not x[0].startswith("__amd_rocclr")):
+                v = sq[(k, c)]
+                fh.write(f"{k:28s} {c:24s} {sum(v) / len(v):18.1f}\n")
     with open(os.path.join(prof, f"{t}_pmc.csv"), "w", newline="") as fh:
         w = csv.writer(fh)
         w.writerow(["kernel", "launches", "FETCH_SIZE_KiB_mean", "WRITE_SIZE_KiB_mean",
