@@ -71,6 +71,9 @@ struct surfhip_detector {
     hipEvent_t fork2 = nullptr;
     float* resp = nullptr;
     uint32_t* colsum = nullptr;
+    // plan.iiw: k_ii_rowseg's row sums of the batch (or of the next batch,
+    // prefetched) that k_hess_w adds to its strip integrals
+    uint32_t* rowseg = nullptr;
     surfhip_point* cand = nullptr;
     uint32_t* keys = nullptr;
     uint64_t* gscratch = nullptr;
@@ -415,7 +418,7 @@ static int derive(surfhip_detector* d)
 
 static void free_all(surfhip_detector* d)
 {
-    void* ptrs[] = {d->d_oct, d->iib[0], d->iib[1], d->resp, d->colsum, d->cand, d->keys, d->gscratch, d->cand_count,
+    void* ptrs[] = {d->d_oct, d->iib[0], d->iib[1], d->resp, d->colsum, d->rowseg, d->cand, d->keys, d->gscratch, d->cand_count,
                     d->scan_key, d->scan_src, d->scan_cube, d->item_count, d->item_off,
                     d->offsets, d->order, d->work, d->status, d->pts1, d->desc1, d->count1, d->dbl};
     for (void* p : ptrs)
@@ -486,6 +489,11 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
         if (e != hipSuccess) goto fail;                      \
     } while (0)
     make_plan(d->P, d->oct, d->plan, max_batch);
+    if (d->plan.iiw) {
+        // the stage also writes the integral image (read: the u8 frame)
+        d->hess_bytes += (long long)d->W * d->H;
+        ALLOC(d->rowseg, B * d->plan.hw_nstrips * d->plan.rs_rows * sizeof(uint32_t));
+    }
     ALLOC(d->d_oct, sizeof(OctaveParams) * kMaxOct);
     ALLOC(d->iib[0], B * d->P.ii_stride * sizeof(int32_t));
     d->ii = d->iib[0];
@@ -521,6 +529,9 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     if (e == hipSuccess) e = hipMemset(d->iib[0], 0, B * d->P.ii_stride * sizeof(int32_t));
     if (e == hipSuccess) e = hipMemset(d->resp, 0, B * d->tot_osize * sizeof(float));
     if (e == hipSuccess) e = hipMemset(d->status, 0, 16);
+    // strip 0's slab and the rows past H stay zero (k_ii_rowseg never writes them)
+    if (e == hipSuccess && d->rowseg)
+        e = hipMemset(d->rowseg, 0, B * d->plan.hw_nstrips * d->plan.rs_rows * sizeof(uint32_t));
     if (e != hipSuccess) goto fail;
     {
         // LUTs (surf.cpp:358-371) and orientation bins (surf.cpp:83-89); the
@@ -599,6 +610,9 @@ int surfhip_run_integral(surfhip_detector* d, const uint8_t* frames, int nframes
     HIPCHK(hipStreamWaitEvent(d->stream, d->join, 0));
     HIPCHK(source_frames(d, frames, pitch, stride, nframes, d->stream));
     HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, d->stream));
+    // (plan.iiw) the row sums a following run_hessian's k_hess_w adds: it
+    // rewrites the same integral image
+    HIPCHK(launch_rowseg(frames, pitch, (long long)stride, nframes, d->P, d->plan, d->rowseg, d->stream));
     d->pref_valid = false;
     d->last_frames = frames;
     d->last_pitch = pitch;
@@ -612,7 +626,7 @@ int surfhip_run_hessian(surfhip_detector* d, int nframes)
     // the u8 Hessian kernels read the frames of the last run_integral
     if (!d->last_frames && plan_reads_frames(d->plan)) return SURFHIP_ERR_INVALID;
     HIPCHK(launch_hessian(d->last_frames, d->last_pitch, d->last_fstride, d->ii, d->resp, nframes, d->P, d->d_oct,
-                          d->oct, d->plan, d->stream));
+                          d->oct, d->plan, d->stream, 3, d->rowseg, d->ii));
     return SURFHIP_OK;
 }
 
@@ -641,13 +655,16 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
         rc = check_frames(d, next_frames, next_nframes, next_pitch, next_stride);
         if (rc) return rc;
     }
-    if (pipe) HIPCHK(ensure_second_ii(d));
+    // (plan.iiw: the integral is written by this batch's Hessian, one buffer)
+    const bool iiw = d->plan.iiw != 0;
+    if (pipe && !iiw) HIPCHK(ensure_second_ii(d));
     hipStream_t s = d->stream;
     const bool prof = d->profiling;
-    // this batch's integral: prefetched by the previous call (same frames), or computed now
+    // this batch's integral (iiw: its row sums): prefetched by the previous
+    // call (same frames), or computed now
     const bool have = !prof && d->pref_valid && d->pref_frames == frames && d->pref_n == nframes &&
                       d->pref_pitch == pitch && d->pref_stride == stride;
-    d->icur = have ? d->ipref : d->icur;
+    d->icur = (have && !iiw) ? d->ipref : (iiw ? 0 : d->icur);
     d->ii = d->iib[d->icur];
     d->pref_valid = false;
     HIPCHK(hipMemsetAsync(d->cand_count, 0, sizeof(int) * nframes, s));
@@ -661,10 +678,11 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
         HIPCHK(hipStreamWaitEvent(s, d->join, 0));
         HIPCHK(hipEventRecord(d->ev[0], s));
         HIPCHK(source_frames(d, frames, pitch, stride, nframes, s));
-        HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, s));
+        if (iiw) HIPCHK(launch_rowseg(frames, pitch, (long long)stride, nframes, d->P, d->plan, d->rowseg, s));
+        else HIPCHK(launch_integral(frames, pitch, (long long)stride, nframes, d->P, d->colsum, d->ii, s));
         HIPCHK(hipEventRecord(d->ev[1], s));
         HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
-                              d->plan, s));
+                              d->plan, s, 3, d->rowseg, d->ii));
         HIPCHK(hipEventRecord(d->ev[2], s));
     } else {
         // In-step Hessian timing brackets the WHOLE stage: from the fork (on
@@ -675,6 +693,22 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
         // bracket then includes.
         HIPCHK(source_frames(d, frames, pitch, stride, nframes, s));
         const bool th = d->time_hess && d->hev_n < SURFHIP_MAX_HESS_EV;
+        if (iiw) {
+            // every octave on the u8 kernels, the integral image written by
+            // k_hess_w: one stream.  Its row sums (unless prefetched) first;
+            // the side stream's last work (a prefetch into d->rowseg) is
+            // ordered before them.
+            HIPCHK(hipEventRecord(d->join, d->side));
+            HIPCHK(hipStreamWaitEvent(s, d->join, 0));
+            if (!have) HIPCHK(launch_rowseg(frames, pitch, (long long)stride, nframes, d->P, d->plan, d->rowseg, s));
+            if (th) HIPCHK(hipEventRecord(d->hev[d->hev_n][0], s));
+            HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
+                                  d->plan, s, 3, d->rowseg, d->ii));
+            if (th) {
+                HIPCHK(hipEventRecord(d->hev[d->hev_n][1], s));
+                d->hev_side[d->hev_n++] = false;
+            }
+        } else {
         if (th) HIPCHK(hipEventRecord(d->hev[d->hev_n][0], s));
         if (!plan_reads_frames(d->plan)) {
             // Every Hessian kernel reads the integral image (the gather plan
@@ -716,18 +750,25 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
             }
             HIPCHK(hipStreamWaitEvent(s, d->join, 0));
         }
+        }
     }
     // The next batch's integral (into the other buffer) on the side stream,
     // ordered after everything on s so far, so that buffer's last readers
     // (the previous batch's fit and describe) are done.  Default: forked
     // after this batch's Hessian, beside its NMS scan, fit and sort (the
     // Hessian and describe then run alone); SURFHIP_PREFETCH=describe forks
-    // it after the sort instead, beside describe.
+    // it after the sort instead, beside describe.  With the integral written
+    // by k_hess_w (iiw) the prefetch is only the row-sum pass and the default
+    // is beside describe (its HBM use is low and its waves leave room).
     auto prefetch_next = [&]() -> hipError_t {
         const int nx = d->icur ^ 1;
         hipError_t e = hipEventRecord(d->fork2, s);
         if (e == hipSuccess) e = hipStreamWaitEvent(d->side, d->fork2, 0);
-        if (e == hipSuccess)
+        // (iiw: the next batch's row sums; this batch's k_hess_w has read d->rowseg)
+        if (e == hipSuccess && iiw)
+            e = launch_rowseg(next_frames, next_pitch, (long long)next_stride, next_nframes, d->P, d->plan,
+                              d->rowseg, d->side);
+        else if (e == hipSuccess)
             e = launch_integral(next_frames, next_pitch, (long long)next_stride, next_nframes, d->P, d->colsum,
                                 d->iib[nx], d->side);
         if (e != hipSuccess) return e;
@@ -739,10 +780,13 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
         d->pref_stride = next_stride;
         return hipSuccess;
     };
-    static const bool pref_nms = [] {
+    // (iiw: the prefetch is the row-sum pass, default beside describe, whose
+    // waves leave room for its 16-VGPR waves; SURFHIP_PREFETCH=nms / describe)
+    static const int pref_env = [] {
         const char* e = getenv("SURFHIP_PREFETCH");
-        return !(e && !strcmp(e, "describe"));
+        return !e ? -1 : !strcmp(e, "describe") ? 0 : 1;
     }();
+    const bool pref_nms = pref_env < 0 ? !iiw : pref_env == 1;
     if (pipe && pref_nms) HIPCHK(prefetch_next());
     HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->scan_key, d->scan_src, d->scan_cube,
                       d->item_count,
@@ -754,7 +798,7 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
     if (pipe && !pref_nms) HIPCHK(prefetch_next());
     if (desc)
         HIPCHK(launch_describe(d->ii, d->P, points, d->max_pts, counts, d->offsets, d->order, d->work, nframes, desc,
-                               d->status + 64, s, pipe && !pref_nms, d->cus));
+                               d->status + 64, s, pipe && !pref_nms && !iiw, d->cus));
     if (prof) HIPCHK(hipEventRecord(d->ev[5], s));
     d->last_nframes = nframes;
     d->last_frames = frames;

@@ -543,6 +543,59 @@ __device__ __forceinline__ float hessian_at(const uint32_t* __restrict__ I, int 
 #include "surfhip_hess_p0.inc"
 #include "surfhip_hess_w.inc"
 
+// The row sums k_hess_w's strips add to their local integral when they write
+// the integral image (plan.iiw): strip k's local integral starts at its halo
+// column cs_k = 480 k - 144, so the image's integral is L_k(R, c) + II(R,
+// cs_k), and II(R, cs_k) is the running sum over pixel rows r < R of S_k(r) =
+// the sum of row r over columns [0, cs_k).  One wave per pixel row: a wave
+// scan of the row's dword sums, chunk by chunk with a running carry; the lane
+// holding the last dword before cs_k stores S_k(r).  Reads columns [0,
+// cs_{ns-1}) of the frame once (1,296 of 1,920 at 1080p).
+// (16 VGPRs: its waves fit beside k_describe_u2's, which leave 20 of a SIMD
+// lane's 512 free, so the pass of the next batch runs inside describe)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(16))) void k_ii_rowseg(
+    const uint8_t* __restrict__ frames, int pitch, long long fstride, int H, int ns, int rs_rows,
+    uint32_t* __restrict__ rowseg)
+{
+    const int f = blockIdx.y;
+    const int r = blockIdx.x * 4 + (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (r >= H) return;
+    const int lane = (int)lane_id();
+    const int nd = (hw::ST * (ns - 1) - hw::H) / 4;          // dwords below the last boundary
+    // the row's dwords [0, nd): a buffer load past them returns 0
+    const rsrc_t R = make_rsrc(frames + (size_t)f * fstride + (size_t)r * pitch, (long long)nd * 4);
+    uint32_t* out = rowseg + (size_t)f * ns * rs_rows + r;
+    uint32_t carry = 0u;
+    constexpr int KC = 6;                                      // loads in flight per lane
+    for (int d0 = 0; d0 < nd; d0 += 64 * KC) {
+        uint32_t v[KC];
+#pragma unroll
+        for (int i = 0; i < KC; i++)
+            v[i] = __builtin_amdgcn_raw_buffer_load_b32(R, (uint32_t)(d0 + 64 * i + lane) * 4u, 0, 0);
+#pragma unroll
+        for (int i = 0; i < KC; i++) {
+            const int d = d0 + 64 * i + lane;
+            const uint32_t x = __builtin_amdgcn_udot4(v[i], 0x01010101u, 0u, false);
+            uint32_t tot;
+            const uint32_t inc = carry + wave_excl_scan(x, tot) + x;
+            carry += tot;
+            // dword d ends at column 4 d + 3: the last one below cs_k when
+            // 4 (d + 1) = 480 k - 144, i.e. d + 37 = 120 k
+            if (d < nd && (d + 37) % (hw::ST / 4) == 0) out[(size_t)((d + 37) / (hw::ST / 4)) * rs_rows] = inc;
+        }
+    }
+}
+
+hipError_t launch_rowseg(const uint8_t* frames, int pitch, long long fstride, int nframes, const FrameParams& P,
+                         const LaunchPlan& plan, uint32_t* rowseg, hipStream_t s)
+{
+    if (!plan.iiw) return hipSuccess;
+    if (plan.hw_nstrips > 1)
+        k_ii_rowseg<<<dim3((P.H + 3) / 4, nframes), 256, 0, s>>>(frames, pitch, fstride, P.H, plan.hw_nstrips,
+                                                                  plan.rs_rows, rowseg);
+    return hipGetLastError();
+}
+
 // Octave 1 on k_hess_q1 (only when k_hess_w is off: 2-octave detectors or
 // SURFHIP_HESS_W=0) needs the geometry compiled into it (sampling 2, lobes
 // 15/19/23).
@@ -655,6 +708,13 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
     }
     plan.hess_start[kMaxOct] = hb;
     plan.nms_start[kMaxOct] = nb;
+    // the integral image from k_hess_w (SURFHIP_II_FUSE=0 disables): every
+    // octave on the u8 kernels, octave 0 on k_hess_p0
+    {
+        const char* fe = getenv("SURFHIP_II_FUSE");
+        plan.iiw = plan.hw_n >= 2 && plan.p0 != 0 && hb == 0 && !plan.t0 && !(fe && atoi(fe) == 0);
+        plan.rs_rows = 4 * plan.hw_nblk;
+    }
 }
 
 std::string hessian_plan_text(const LaunchPlan& plan, const FrameParams& P)
@@ -676,6 +736,9 @@ std::string hessian_plan_text(const LaunchPlan& plan, const FrameParams& P)
     }
     if (plan.t0) add("k_hessian_t0", 0, 0);
     if (plan.hw_n > 0) add("k_hess_w", 1, plan.hw_n);
+    // (the row-sum pass runs before the stage: beside the previous batch's
+    // NMS when pipelined, like the integral passes it replaces)
+    if (plan.iiw) t += ", writing the integral image";
     if (plan.hess_start[kMaxOct] > 0) {
         int lo = -1, hi = -1;
         for (int o = 0; o < P.noct; o++)
@@ -799,7 +862,7 @@ __global__ __launch_bounds__(256) void k_hessian_t0(const int32_t* __restrict__ 
 
 hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, const int32_t* ii, float* resp,
                           int nframes, const FrameParams& P, const OctaveParams* d_oct, const OctaveParams* h_oct,
-                          const LaunchPlan& plan, hipStream_t s, int parts)
+                          const LaunchPlan& plan, hipStream_t s, int parts, const uint32_t* rowseg, int32_t* ii_out)
 {
     const int nf8 = (nframes + 7) & ~7;
     // parts: 1 = the kernels that read the u8 frames, 2 = those that read the
@@ -831,12 +894,18 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
         if (plan.hw_n > 0) {
             const dim3 g(nf8 * plan.hw_nstrips);
             const OctaveParams& q3 = h_oct[plan.hw_n >= 3 ? 3 : 2];
-            if (plan.hw_n >= 3)
-                k_hess_w<3><<<g, hw::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[1], h_oct[2], q3,
-                                                      plan.hw_nstrips, nframes, plan.hw_nblk);
-            else
-                k_hess_w<2><<<g, hw::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[1], h_oct[2], q3,
-                                                      plan.hw_nstrips, nframes, plan.hw_nblk);
+            const bool wr = plan.iiw && ii_out && rowseg;
+#define HW_LAUNCH(NO, IIW)                                                                                       \
+    k_hess_w<NO, IIW><<<g, hw::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[1], h_oct[2], q3,          \
+                                                plan.hw_nstrips, nframes, plan.hw_nblk, rowseg, ii_out, plan.rs_rows)
+            if (plan.hw_n >= 3) {
+                if (wr) HW_LAUNCH(3, true);
+                else HW_LAUNCH(3, false);
+            } else {
+                if (wr) HW_LAUNCH(2, true);
+                else HW_LAUNCH(2, false);
+            }
+#undef HW_LAUNCH
         }
     }
     if (plan.t0 && iip)

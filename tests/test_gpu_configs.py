@@ -351,3 +351,62 @@ def test_run_hessian_without_integral(surf):
     with pytest.raises(surf.SurfError, match="invalid argument"):
         det.run_hessian(16)
     det.close()
+
+
+@pytest.mark.parametrize("w,h", [(960, 130), (1001, 97), (1002, 64), (1003, 71), (481, 50), (1920, 1080)])
+def test_fused_integral_from_hessian(surf, orc, w, h):
+    """plan.iiw: k_hess_w's producers write the integral image (their strip
+    integral plus k_ii_rowseg's row sums left of the strip), no separate
+    integral pass.  Bit-exact against the oracle for widths on and off the
+    480-column strip grid and every W % 4 (the lane holding column W stores
+    only columns <= W; the pad columns stay 0), through detect_batch and
+    through the pipelined entry point (row sums prefetched by the previous
+    call)."""
+    n = 3
+    frames = surf.synth_frames(n, w, h, first=900)
+    pitch = frames.shape[2]
+    param = surf.make_param(4, 4.0, upright=True)
+    det = surf.Detector(param, w, h, max_batch=n, max_pts=4096)
+    assert "writing the integral image" in det.hessian_kernels()
+    fb = [surf.DeviceBuffer(frames.nbytes) for _ in range(2)]
+    fb[0].upload(frames)
+    fb[1].upload(frames[::-1].copy())
+    pb = surf.DeviceBuffer(48 * n * 4096)
+    cb = surf.DeviceBuffer(4 * n)
+    ip = surf.align_up(w + 1, 128)
+
+    def check(order):
+        surf.synchronize()
+        ii, iis, _, _ = det.workspace()
+        got = surf.download_ptr(ii, np.int32, n * iis).reshape(n, -1)
+        for f in range(n):
+            ref = orc.integral(frames[order[f]], w, h)
+            assert np.array_equal(got[f][: (h + 1) * ip].reshape(h + 1, ip), ref), (w, h, f)
+
+    det.detect_batch(fb[0].ptr, n, pitch, h * pitch, pb.ptr, None, cb.ptr)
+    check([0, 1, 2])
+    det.detect_batch_next(fb[1].ptr, n, pitch, h * pitch, pb.ptr, None, cb.ptr, fb[0].ptr, n, pitch, h * pitch)
+    check([2, 1, 0])
+    det.detect_batch_next(fb[0].ptr, n, pitch, h * pitch, pb.ptr, None, cb.ptr, None, 0, 0, 0)
+    check([0, 1, 2])
+    det.close()
+
+
+def test_fused_integral_switch(surf, monkeypatch):
+    """SURFHIP_II_FUSE=0 keeps the separate integral passes (A/B); the gather
+    plan (few frames) and 5-octave plans (k_hessian reads the integral) never
+    fuse."""
+    param = surf.make_param(4, 4.0, upright=True)
+    monkeypatch.setenv("SURFHIP_II_FUSE", "0")
+    det = surf.Detector(param, 640, 480, max_batch=16, max_pts=1024)
+    assert "integral" not in det.hessian_kernels()
+    det.close()
+    monkeypatch.delenv("SURFHIP_II_FUSE")
+    monkeypatch.setenv("SURFHIP_HESS_GATHER", "1")
+    det = surf.Detector(param, 640, 480, max_batch=16, max_pts=1024)
+    assert "integral" not in det.hessian_kernels()
+    det.close()
+    monkeypatch.setenv("SURFHIP_HESS_GATHER", "0")
+    det = surf.Detector(surf.make_param(5, 4.0, upright=True), 1920, 1080, max_batch=16, max_pts=1024)
+    assert "integral" not in det.hessian_kernels()
+    det.close()

@@ -5,7 +5,7 @@
 # value, ms/step, the Hessian stage (in-step events and serial), describe.
 #   bash tools/ab.sh <tag> "<variant> <variant> ..." [pairs] [bench args...]
 # variant: "default" (cuda-surf_amd/) or a diag build name (cuda-surf_amd/diag/<name>,
-# tools/diag_build.sh); an "env:NAME=VAL" variant runs the default build with that env.
+# tools/diag_build.sh); an "env:NAME=VAL[,NAME=VAL]" variant runs the default build with that env.
 set -u
 TAG=$1; VARS=$2; PAIRS=${3:-2}; shift 3 2>/dev/null || shift $#
 cd /tmp && export TMPDIR=/tmp
@@ -17,7 +17,7 @@ for r in $(seq 1 $PAIRS); do
     EV=(); LD=cuda-surf_amd
     case $v in
       default) ;;
-      env:*) EV=("${v#env:}") ;;
+      env:*) IFS=, read -ra EV <<< "${v#env:}" ;;
       *) LD=cuda-surf_amd/diag/$v ;;
     esac
     n=$(echo "$v" | tr -c 'A-Za-z0-9_\n' '_')

@@ -32,7 +32,7 @@ for _ in range(4):
     det.detect_batch(buf.ptr, B, pitch, H * pitch, pb.ptr, db.ptr, cb.ptr)
 surf.synchronize()
 lib = C.CDLL(os.path.join(os.environ["SURFHIP_LIB_DIR"], "libsurfhip.so"))
-st = np.zeros((8192, 9), np.uint64)
+st = np.zeros((8192, 12), np.uint64)
 assert lib.surfhip_diag_u2_stamps(st.ctypes.data_as(C.c_void_p)) == 0
 st = st.astype(np.float64)
 tot = st.sum(axis=0)
@@ -44,3 +44,6 @@ for i, nm in enumerate(names):
     per = tot[i] / max(1, (tot[5 + i] if 1 <= i <= 3 else n))
     print(f"{nm:13s} {tot[i] / allt * 100:5.1f} %   {per:9.1f} ticks per keypoint (of its kind)")
 print(f"all phases {allt / n:.1f} ticks per keypoint per wave")
+print(f"seg: first ring wait {tot[9] / max(1, tot[6]):.1f} ticks per keypoint; narrow (W4 <= 16) "
+      f"{int(tot[10])} keypoints, rows {tot[11] / max(1, tot[10]):.1f} ticks; wide "
+      f"{int(tot[6] - tot[10])}, rows {(tot[1] - tot[11]) / max(1, tot[6] - tot[10]):.1f} ticks")
