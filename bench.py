@@ -610,7 +610,10 @@ def run_rank(args):
                          "launch_ms_source": ("in-step: HIP events from the Hessian's fork to the end of its "
                                               "last kernel on either stream, in "
                                               f"{len(hess_instep)} pipelined steps run after the timed region, "
-                                              + ("the batch's own integral beside them" if args.no_pipeline else
+                                              + ("k_hess_w writing the batch's integral image, the next "
+                                                 "batch's row-sum pass beside describe"
+                                                 if "writing the integral image" in kern else
+                                                 "the batch's own integral beside them" if args.no_pipeline else
                                                  "the next batch's integral beside the NMS stage instead")
                                               if hess_instep else "serial"),
                          "launch_ms_serial": round(hess_serial_ms, 4)},
