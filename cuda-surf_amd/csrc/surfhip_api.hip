@@ -694,8 +694,9 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
         HIPCHK(source_frames(d, frames, pitch, stride, nframes, s));
         const bool th = d->time_hess && d->hev_n < SURFHIP_MAX_HESS_EV;
         if (iiw) {
-            // every octave on the u8 kernels, the integral image written by
-            // k_hess_w: one stream.  Its row sums (unless prefetched) first;
+            // octaves 0-3 on the u8 kernels, the integral image written by
+            // k_hess_w, any later octave's k_hessian after them (it reads
+            // that integral): one stream.  Its row sums (unless prefetched) first;
             // the side stream's last work (a prefetch into d->rowseg) is
             // ordered before them.
             HIPCHK(hipEventRecord(d->join, d->side));

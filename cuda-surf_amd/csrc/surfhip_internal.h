@@ -120,7 +120,8 @@ struct LaunchPlan {
     int t0, t0_nbx, t0_nby;         // octave 0 of the gather plan on k_hessian_t0 (LDS tiles): its blocks
     // k_hess_w also writes the integral image (its producers' strip integral
     // plus the row sums left of the strip, k_ii_rowseg): no separate integral
-    // pass.  Set when every octave is on the u8 kernels (p0 + k_hess_w).
+    // pass.  Set when octaves 0-3 are on the u8 kernels (p0 + k_hess_w);
+    // k_hessian octaves (past 3) run after them on the same stream.
     int iiw;
     int rs_rows;                    // rows per rowseg slab (4 x hw_nblk, zero past H)
 };

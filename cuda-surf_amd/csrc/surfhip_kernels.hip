@@ -708,11 +708,12 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
     }
     plan.hess_start[kMaxOct] = hb;
     plan.nms_start[kMaxOct] = nb;
-    // the integral image from k_hess_w (SURFHIP_II_FUSE=0 disables): every
-    // octave on the u8 kernels, octave 0 on k_hess_p0
+    // the integral image from k_hess_w (SURFHIP_II_FUSE=0 disables): octave
+    // 0 on k_hess_p0 and octaves 1-3 on k_hess_w; octaves past 3 (k_hessian)
+    // then read the integral k_hess_w wrote, after it on the same stream
     {
         const char* fe = getenv("SURFHIP_II_FUSE");
-        plan.iiw = plan.hw_n >= 2 && plan.p0 != 0 && hb == 0 && !plan.t0 && !(fe && atoi(fe) == 0);
+        plan.iiw = plan.hw_n >= 2 && plan.p0 != 0 && !plan.t0 && !(fe && atoi(fe) == 0);
         plan.rs_rows = 4 * plan.hw_nblk;
     }
 }

@@ -394,8 +394,8 @@ def test_fused_integral_from_hessian(surf, orc, w, h):
 
 def test_fused_integral_switch(surf, monkeypatch):
     """SURFHIP_II_FUSE=0 keeps the separate integral passes (A/B); the gather
-    plan (few frames) and 5-octave plans (k_hessian reads the integral) never
-    fuse."""
+    plan (few frames) never fuses; a 5-octave plan does (octave 4's k_hessian
+    reads the integral k_hess_w wrote, after it on the same stream)."""
     param = surf.make_param(4, 4.0, upright=True)
     monkeypatch.setenv("SURFHIP_II_FUSE", "0")
     det = surf.Detector(param, 640, 480, max_batch=16, max_pts=1024)
@@ -408,5 +408,5 @@ def test_fused_integral_switch(surf, monkeypatch):
     det.close()
     monkeypatch.setenv("SURFHIP_HESS_GATHER", "0")
     det = surf.Detector(surf.make_param(5, 4.0, upright=True), 1920, 1080, max_batch=16, max_pts=1024)
-    assert "integral" not in det.hessian_kernels()
+    assert "writing the integral image" in det.hessian_kernels() and "k_hessian (octave 4)" in det.hessian_kernels()
     det.close()
