@@ -667,9 +667,9 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
     d->icur = (have && !iiw) ? d->ipref : (iiw ? 0 : d->icur);
     d->ii = d->iib[d->icur];
     d->pref_valid = false;
-    HIPCHK(hipMemsetAsync(d->cand_count, 0, sizeof(int) * nframes, s));
-    HIPCHK(hipMemsetAsync(d->status, 0, sizeof(int), s));       // per-batch truncation flag
-    HIPCHK(hipMemsetAsync(d->item_count, 0, sizeof(int) * (size_t)nframes * d->nitems, s));
+    // (the per-batch counters -- accepted candidates per frame, the
+    // truncation flag, the scan items' survivor counts -- are written by the
+    // NMS scan itself: no memsets ahead of the Hessian)
     if (prof) {
         // serial, so that the stage events bracket each stage alone; a
         // prefetch left on the side stream by an earlier pipelined call may
@@ -791,7 +791,7 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
     if (pipe && pref_nms) HIPCHK(prefetch_next());
     HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->scan_key, d->scan_src, d->scan_cube,
                       d->item_count,
-                      d->item_off, d->cand, d->keys, d->cand_count, d->cap, s));
+                      d->item_off, d->cand, d->keys, d->cand_count, d->cap, d->status, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[3], s));
     HIPCHK(launch_sort(d->cand, d->keys, d->gscratch, d->cand_count, d->item_off, d->plan.nms_start[kMaxOct] * 4,
                        d->cap, nframes, points, d->max_pts, counts, d->offsets, d->order, d->status, s));

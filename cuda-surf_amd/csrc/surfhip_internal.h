@@ -151,10 +151,11 @@ hipError_t launch_rowseg(const uint8_t* frames, int pitch, long long fstride, in
                          const LaunchPlan& plan, uint32_t* rowseg, hipStream_t s);
 // NMS scan items: one wave's 64 block columns x kScanRows / 4 block rows;
 // each item owns kItemCap survivor slots (no atomics in the scan).
+// (also zeroes cand_count[0, nframes) and *status, the per-batch counters)
 hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,
                       const OctaveParams* d_oct, const LaunchPlan& plan, uint32_t* scan_key, uint32_t* scan_src,
                       float* scan_cube, int* item_count, int* item_off, surfhip_point* cand, uint32_t* keys,
-                      int* cand_count, int cap, hipStream_t s);
+                      int* cand_count, int cap, int* status, hipStream_t s);
 hipError_t launch_sort(const surfhip_point* cand, const uint32_t* keys, uint64_t* gscratch,
                        const int* cand_count, const int* soff, int items_per_frame, int cap, int nframes,
                        surfhip_point* out, int max_pts, int* out_count, int* offsets, int* order, int* status,

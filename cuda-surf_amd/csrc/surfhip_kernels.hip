@@ -1412,7 +1412,8 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
         }
         wave_sync();                          // sbest / sinfo are rewritten by the next pass
     });
-    if (lane_id() == 0u && nsurv > 0) item_count[item] = nsurv;
+    // every item writes its count, zero included (no per-batch memset)
+    if (lane_id() == 0u) item_count[item] = nsurv;
 }
 
 // CUBE: write the survivors' fit records (k_nms_fit's first pass then reads
@@ -1423,13 +1424,19 @@ __global__ __launch_bounds__(256) void k_nms_scan(const float* __restrict__ resp
                                                   const OctaveParams* __restrict__ oct, LaunchPlan plan,
                                                   uint32_t* __restrict__ scan_key, uint32_t* __restrict__ scan_src,
                                                   float* __restrict__ scan_cube, int* __restrict__ item_count,
-                                                  int nframes)
+                                                  int nframes, int* __restrict__ cand_count, int* __restrict__ status)
 {
     __shared__ float sbest[4][64 * 4];                // one pass's candidates per wave
     __shared__ __attribute__((aligned(16))) float sblk[4][64 * 8];   // blocks of its first 64 (CUBE)
     __shared__ uint32_t sinfo[4][64 * 4];
     int f, gb;
     if (!xcd_frame_block(plan.nms_start[kMaxOct], nframes, f, gb)) return;
+    // the batch's counters the fit and sort use after this kernel: the
+    // frame's accepted-candidate count and the truncation flag (no memsets)
+    if (gb == 0 && threadIdx.x == 0) {
+        cand_count[f] = 0;
+        if (f == 0) *status = 0;
+    }
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // plane k (= 2 z + 1) is a halfImage view for octaves > 0 at level z = 0
     const int o = octave_of(plan.nms_start, P.noct, gb);
@@ -1592,10 +1599,15 @@ __global__ __launch_bounds__(256) void k_nms_fit(const int32_t* __restrict__ ii,
 hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,
                       const OctaveParams* d_oct, const LaunchPlan& plan, uint32_t* scan_key, uint32_t* scan_src,
                       float* scan_cube, int* item_count, int* item_off, surfhip_point* cand, uint32_t* keys,
-                      int* cand_count, int cap, hipStream_t s)
+                      int* cand_count, int cap, int* status, hipStream_t s)
 {
     const int per = plan.nms_start[kMaxOct];
-    if (per == 0) return hipSuccess;
+    if (per == 0) {
+        // (no NMS level: nothing to scan; the counters the sort reads are 0)
+        hipError_t e = hipMemsetAsync(cand_count, 0, sizeof(int) * (size_t)nframes, s);
+        if (e == hipSuccess) e = hipMemsetAsync(status, 0, sizeof(int), s);
+        return e;
+    }
     // the scan's fit records for every batch size (round 5: one 1080p frame's
     // NMS 0.038 -> 0.034 ms with them; round 2's cross-lane variant had made
     // single frames slower)
@@ -1604,7 +1616,7 @@ hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const F
     if (!cube) scan_cube = nullptr;
     auto* scan = cube ? &k_nms_scan<true> : &k_nms_scan<false>;
     scan<<<dim3(frame_grid(nframes) * per), 256, 0, s>>>(resp, P, d_oct, plan, scan_key, scan_src, scan_cube,
-                                                                item_count, nframes);
+                                                                item_count, nframes, cand_count, status);
     const int nitems = nframes * per * 4;
     launch_excl_scan(item_count, nitems, item_off, item_off + nitems + 1, s);
     k_nms_fit<<<fit_grid(), 256, 0, s>>>(ii, resp, P, d_oct, scan_key, scan_src, scan_cube, item_off, nitems, per * 4,
