@@ -696,15 +696,22 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
         if (iiw) {
             // octaves 0-3 on the u8 kernels, the integral image written by
             // k_hess_w, any later octave's k_hessian after them (it reads
-            // that integral): one stream.  Its row sums (unless prefetched) first;
-            // the side stream's last work (a prefetch into d->rowseg) is
-            // ordered before them.
+            // that integral): one stream.  The side stream's last work (a
+            // prefetch of d->rowseg) is ordered before the row sums' use:
+            // before this call's own row-sum pass, or, prefetched, between
+            // the octave-0 kernel and k_hess_w, where the wait's latency
+            // hides behind the running octave-0 kernel.
             HIPCHK(hipEventRecord(d->join, d->side));
-            HIPCHK(hipStreamWaitEvent(s, d->join, 0));
-            if (!have) HIPCHK(launch_rowseg(frames, pitch, (long long)stride, nframes, d->P, d->plan, d->rowseg, s));
+            if (!have) {
+                HIPCHK(hipStreamWaitEvent(s, d->join, 0));
+                HIPCHK(launch_rowseg(frames, pitch, (long long)stride, nframes, d->P, d->plan, d->rowseg, s));
+            }
             if (th) HIPCHK(hipEventRecord(d->hev[d->hev_n][0], s));
             HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
-                                  d->plan, s, 3, d->rowseg, d->ii));
+                                  d->plan, s, 4));
+            if (have) HIPCHK(hipStreamWaitEvent(s, d->join, 0));
+            HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
+                                  d->plan, s, 8 | 2, d->rowseg, d->ii));
             if (th) {
                 HIPCHK(hipEventRecord(d->hev[d->hev_n][1], s));
                 d->hev_side[d->hev_n++] = false;

@@ -138,7 +138,8 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
 std::string hessian_plan_text(const LaunchPlan& plan, const FrameParams& P);
 
 // parts: 1 = the u8-frame kernels (frames must be given), 2 = the
-// integral-image kernel (k_hessian), 3 = both.  ii_out + rowseg (plan.iiw):
+// integral-image kernel (k_hessian), 3 = both; 4 / 8 = only the octave-0 /
+// only the k_hess_w launch of part 1.  ii_out + rowseg (plan.iiw):
 // k_hess_w writes the frames' integral image into ii_out (rowseg: the
 // k_ii_rowseg sums of the same frames); nullptr: it does not.
 hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, const int32_t* ii, float* resp,

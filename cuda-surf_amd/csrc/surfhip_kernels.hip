@@ -868,9 +868,29 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
     const int nf8 = (nframes + 7) & ~7;
     // parts: 1 = the kernels that read the u8 frames, 2 = those that read the
     // integral image (the two may run on different streams)
-    const bool u8p = (parts & 1) != 0, iip = (parts & 2) != 0;
+    // (4 / 8: only the octave-0 / only the k_hess_w launch of part 1)
+    const bool p0p = (parts & 5) != 0, wp = (parts & 9) != 0, iip = (parts & 2) != 0;
+    const bool u8p = p0p || wp;
     if (u8p && !frames && (plan.q0 || plan.q1 || plan.hw_n > 0)) return hipErrorInvalidValue;
-    if (u8p) {
+    auto launch_w = [&]() {
+        if (plan.hw_n > 0) {
+            const dim3 g(nf8 * plan.hw_nstrips);
+            const OctaveParams& q3 = h_oct[plan.hw_n >= 3 ? 3 : 2];
+            const bool wr = plan.iiw && ii_out && rowseg;
+#define HW_LAUNCH(NO, IIW)                                                                                       \
+    k_hess_w<NO, IIW><<<g, hw::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[1], h_oct[2], q3,          \
+                                                plan.hw_nstrips, nframes, plan.hw_nblk, rowseg, ii_out, plan.rs_rows)
+            if (plan.hw_n >= 3) {
+                if (wr) HW_LAUNCH(3, true);
+                else HW_LAUNCH(3, false);
+            } else {
+                if (wr) HW_LAUNCH(2, true);
+                else HW_LAUNCH(2, false);
+            }
+#undef HW_LAUNCH
+        }
+    };
+    if (p0p) {
         const int nb0 = 8 * (((nf8 / 8) * plan.q0_strips + q0::WAVES - 1) / q0::WAVES);
         const int nb1 = 8 * (((nf8 / 8) * plan.q1_strips + q1::WAVES - 1) / q1::WAVES);
         if (plan.q01) {
@@ -892,23 +912,8 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
                 k_hess_q1<2><<<dim3(nb1), q1::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[1],
                                                                plan.q1_strips, nframes);
         }
-        if (plan.hw_n > 0) {
-            const dim3 g(nf8 * plan.hw_nstrips);
-            const OctaveParams& q3 = h_oct[plan.hw_n >= 3 ? 3 : 2];
-            const bool wr = plan.iiw && ii_out && rowseg;
-#define HW_LAUNCH(NO, IIW)                                                                                       \
-    k_hess_w<NO, IIW><<<g, hw::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[1], h_oct[2], q3,          \
-                                                plan.hw_nstrips, nframes, plan.hw_nblk, rowseg, ii_out, plan.rs_rows)
-            if (plan.hw_n >= 3) {
-                if (wr) HW_LAUNCH(3, true);
-                else HW_LAUNCH(3, false);
-            } else {
-                if (wr) HW_LAUNCH(2, true);
-                else HW_LAUNCH(2, false);
-            }
-#undef HW_LAUNCH
-        }
     }
+    if (wp) launch_w();
     if (plan.t0 && iip)
         k_hessian_t0<kT0Halo><<<dim3(frame_grid(nframes) * plan.t0_nbx * plan.t0_nby), 256, 0, s>>>(
             ii, resp, P, h_oct[0], plan.t0_nbx, plan.t0_nby, nframes);
