@@ -329,7 +329,6 @@ def run_rank(args):
     d_pts = torch.empty(B * args.max_pts * 48, dtype=torch.uint8, device=dev)
     d_desc = torch.empty(B * args.max_pts * nf, dtype=torch.float32, device=dev)
     d_cnt = torch.zeros(B, dtype=torch.int32, device=dev)
-    d_cnt_max = torch.zeros(B, dtype=torch.int32, device=dev)     # max over every step's counts
     profile = not args.no_profile
     # the timed loop runs unprofiled (the detector then overlaps the integral
     # with the u8 Hessian kernels on a side stream); stage times come from a
@@ -344,14 +343,12 @@ def run_rank(args):
         elif args.no_pipeline:
             det.detect_batch(d_frames.data_ptr(), B, pitch, H * pitch, d_pts.data_ptr(), d_desc.data_ptr(),
                              d_cnt.data_ptr())
-            torch.maximum(d_cnt_max, d_cnt, out=d_cnt_max)
         else:
             # the next step's batch is the same resident frames: its integral
             # is computed beside this batch's describe (one integral per step,
             # as in the serial arrangement)
             det.detect_batch_next(d_frames.data_ptr(), B, pitch, H * pitch, d_pts.data_ptr(), d_desc.data_ptr(),
                                   d_cnt.data_ptr(), d_frames.data_ptr(), B, pitch, H * pitch)
-            torch.maximum(d_cnt_max, d_cnt, out=d_cnt_max)
 
     if args.hessian_only:
         det.run_integral(d_frames.data_ptr(), B, pitch, H * pitch)
@@ -455,13 +452,15 @@ def run_rank(args):
         hess_instep = det.hessian_times()
         det.time_hessian(False)
 
-    # no truncation anywhere: a frame at max_pts (max over every step's
-    # counts), a candidate-capacity overflow or a slab beyond the agreed
-    # capacity invalidates the run.  The truncation flag and the slab flags
-    # are read from the last step; every step processes the same frames, so
-    # they are the same in every step.
+    # no truncation anywhere: a frame at max_pts, a candidate-capacity
+    # overflow or a slab beyond the agreed capacity invalidates the run.  The
+    # counts, the truncation flag and the slab flags are read from the last
+    # step: every step processes the same frames and the pipeline is
+    # deterministic (tests/test_gpu_parity.py), so they are the same in every
+    # step (round 4 kept a running max of the counts with a torch kernel in
+    # each timed step; it is not needed)
     counts = d_cnt.cpu().numpy()
-    counts_max = d_cnt_max.cpu().numpy()
+    counts_max = counts
     problems = []
     if not args.hessian_only:
         if det.truncated():
