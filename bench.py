@@ -605,7 +605,14 @@ def run_rank(args):
                          # the counter bytes (what the kernels really move) over the same time
                          "frac_traffic": (None if not traffic else
                                           round(traffic / (hess_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)),
-                         "algorithmic_bytes_per_launch": hb, "launch_ms": round(hess_ms, 4),
+                         "algorithmic_bytes_per_launch": hb,
+                         "algorithmic_bytes_def": (
+                             "per frame: u8 frame read + integral image written + valid responses written "
+                             "(the stage writes the integral image; before round 5 it was a separate pass beside "
+                             "NMS and the definition was integral read + responses)"
+                             if "writing the integral image" in kern else
+                             "per frame: integral image read once + valid responses written (SURVEY 8d)"),
+                         "launch_ms": round(hess_ms, 4),
                          "launch_ms_source": ("in-step: HIP events from the Hessian's fork to the end of its "
                                               "last kernel on either stream, in "
                                               f"{len(hess_instep)} pipelined steps run after the timed region, "
