@@ -492,7 +492,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     if (d->plan.iiw) {
         // the stage also writes the integral image (read: the u8 frame)
         d->hess_bytes += (long long)d->W * d->H;
-        ALLOC(d->rowseg, B * d->plan.hw_nstrips * d->plan.rs_rows * sizeof(uint32_t));
+        ALLOC(d->rowseg, B * d->plan.rs_nstrips * d->plan.rs_rows * sizeof(uint32_t));
     }
     ALLOC(d->d_oct, sizeof(OctaveParams) * kMaxOct);
     ALLOC(d->iib[0], B * d->P.ii_stride * sizeof(int32_t));
@@ -531,7 +531,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     if (e == hipSuccess) e = hipMemset(d->status, 0, 16);
     // strip 0's slab and the rows past H stay zero (k_ii_rowseg never writes them)
     if (e == hipSuccess && d->rowseg)
-        e = hipMemset(d->rowseg, 0, B * d->plan.hw_nstrips * d->plan.rs_rows * sizeof(uint32_t));
+        e = hipMemset(d->rowseg, 0, B * d->plan.rs_nstrips * d->plan.rs_rows * sizeof(uint32_t));
     if (e != hipSuccess) goto fail;
     {
         // LUTs (surf.cpp:358-371) and orientation bins (surf.cpp:83-89); the
@@ -700,16 +700,17 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
             // prefetch of d->rowseg) is ordered before the row sums' use:
             // before this call's own row-sum pass, or, prefetched, between
             // the octave-0 kernel and k_hess_w, where the wait's latency
-            // hides behind the running octave-0 kernel.
+            // hides behind the running octave-0 kernel (iiw 2: the octave-0
+            // kernel writes the integral, so the wait precedes it).
+            const bool p0w = d->plan.iiw == 2;
             HIPCHK(hipEventRecord(d->join, d->side));
-            if (!have) {
-                HIPCHK(hipStreamWaitEvent(s, d->join, 0));
+            if (!have || p0w) HIPCHK(hipStreamWaitEvent(s, d->join, 0));
+            if (!have)
                 HIPCHK(launch_rowseg(frames, pitch, (long long)stride, nframes, d->P, d->plan, d->rowseg, s));
-            }
             if (th) HIPCHK(hipEventRecord(d->hev[d->hev_n][0], s));
             HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
-                                  d->plan, s, 4));
-            if (have) HIPCHK(hipStreamWaitEvent(s, d->join, 0));
+                                  d->plan, s, 4, d->rowseg, d->ii));
+            if (have && !p0w) HIPCHK(hipStreamWaitEvent(s, d->join, 0));
             HIPCHK(launch_hessian(frames, pitch, (long long)stride, d->ii, d->resp, nframes, d->P, d->d_oct, d->oct,
                                   d->plan, s, 8 | 2, d->rowseg, d->ii));
             if (th) {

@@ -118,12 +118,15 @@ struct LaunchPlan {
     int hw_n;                       // octaves 1 .. hw_n on k_hess_w (u8, shared strip integral); 0: off
     int hw_nstrips, hw_nblk;        // its strips per frame and blocks of 4 integral rows
     int t0, t0_nbx, t0_nby;         // octave 0 of the gather plan on k_hessian_t0 (LDS tiles): its blocks
-    // k_hess_w also writes the integral image (its producers' strip integral
-    // plus the row sums left of the strip, k_ii_rowseg): no separate integral
-    // pass.  Set when octaves 0-3 are on the u8 kernels (p0 + k_hess_w);
-    // k_hessian octaves (past 3) run after them on the same stream.
+    // A u8 Hessian kernel also writes the integral image (its producers'
+    // strip integral plus the row sums left of the strip, k_ii_rowseg): no
+    // separate integral pass.  Set when octaves 0-3 are on the u8 kernels
+    // (p0 + k_hess_w); k_hessian octaves (past 3) run after them on the same
+    // stream.  1: k_hess_w writes it (480-column strips), 2: k_hess_p0
+    // (128-column strips).
     int iiw;
     int rs_rows;                    // rows per rowseg slab (4 x hw_nblk, zero past H)
+    int rs_nstrips;                 // rowseg slabs per frame: the writer's strips
 };
 // the plan has kernels that read the u8 frames (not only the integral image)
 inline bool plan_reads_frames(const LaunchPlan& p) { return p.q0 || p.q1 || p.hw_n > 0; }
@@ -140,14 +143,15 @@ std::string hessian_plan_text(const LaunchPlan& plan, const FrameParams& P);
 // parts: 1 = the u8-frame kernels (frames must be given), 2 = the
 // integral-image kernel (k_hessian), 3 = both; 4 / 8 = only the octave-0 /
 // only the k_hess_w launch of part 1.  ii_out + rowseg (plan.iiw):
-// k_hess_w writes the frames' integral image into ii_out (rowseg: the
-// k_ii_rowseg sums of the same frames); nullptr: it does not.
+// k_hess_w (iiw 1) or k_hess_p0 (iiw 2) writes the frames' integral image
+// into ii_out (rowseg: the k_ii_rowseg sums of the same frames); nullptr:
+// neither does.
 hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, const int32_t* ii, float* resp,
                           int nframes, const FrameParams& P, const OctaveParams* d_oct, const OctaveParams* h_oct,
                           const LaunchPlan& plan, hipStream_t s, int parts = 3, const uint32_t* rowseg = nullptr,
                           int32_t* ii_out = nullptr);
-// plan.iiw: the row sums k_hess_w's strips add to their integral (rowseg:
-// nframes x hw_nstrips x rs_rows uint32; slab 0 and rows >= H stay zero)
+// plan.iiw: the row sums the writer's strips add to their integral (rowseg:
+// nframes x rs_nstrips x rs_rows uint32; slab 0 and rows >= H stay zero)
 hipError_t launch_rowseg(const uint8_t* frames, int pitch, long long fstride, int nframes, const FrameParams& P,
                          const LaunchPlan& plan, uint32_t* rowseg, hipStream_t s);
 // NMS scan items: one wave's 64 block columns x kScanRows / 4 block rows;

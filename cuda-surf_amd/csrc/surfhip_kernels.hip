@@ -543,25 +543,28 @@ __device__ __forceinline__ float hessian_at(const uint32_t* __restrict__ I, int 
 #include "surfhip_hess_p0.inc"
 #include "surfhip_hess_w.inc"
 
-// The row sums k_hess_w's strips add to their local integral when they write
-// the integral image (plan.iiw): strip k's local integral starts at its halo
-// column cs_k = 480 k - 144, so the image's integral is L_k(R, c) + II(R,
-// cs_k), and II(R, cs_k) is the running sum over pixel rows r < R of S_k(r) =
-// the sum of row r over columns [0, cs_k).  One wave per pixel row: a wave
-// scan of the row's dword sums, chunk by chunk with a running carry; the lane
-// holding the last dword before cs_k stores S_k(r).  Reads columns [0,
-// cs_{ns-1}) of the frame once (1,296 of 1,920 at 1080p).
+// The row sums the integral writer's strips add to their local integral
+// (plan.iiw): strip k's local integral starts at its halo column cs_k = ST k
+// - HALO (k_hess_w: 480 k - 144; k_hess_p0: 128 k - 16), so the image's
+// integral is L_k(R, c) + II(R, cs_k), and II(R, cs_k) is the running sum
+// over pixel rows r < R of S_k(r) = the sum of row r over columns [0, cs_k).
+// One wave per pixel row: a wave scan of the row's dword sums, chunk by chunk
+// with a running carry; the lane holding the last dword before cs_k stores
+// S_k(r).  Reads columns [0, cs_{ns-1}) of the frame once (1,296 of 1,920 at
+// 1080p for k_hess_w's strips).
 // (16 VGPRs: its waves fit beside k_describe_u2's, which leave 20 of a SIMD
 // lane's 512 free, so the pass of the next batch runs inside describe)
+template <int ST, int HALO>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(16))) void k_ii_rowseg(
     const uint8_t* __restrict__ frames, int pitch, long long fstride, int H, int ns, int rs_rows,
     uint32_t* __restrict__ rowseg)
 {
+    static_assert(ST % 4 == 0 && HALO % 4 == 0, "strip boundaries on dword boundaries");
     const int f = blockIdx.y;
     const int r = blockIdx.x * 4 + (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (r >= H) return;
     const int lane = (int)lane_id();
-    const int nd = (hw::ST * (ns - 1) - hw::H) / 4;          // dwords below the last boundary
+    const int nd = (ST * (ns - 1) - HALO) / 4;                // dwords below the last boundary
     // the row's dwords [0, nd): a buffer load past them returns 0
     const rsrc_t R = make_rsrc(frames + (size_t)f * fstride + (size_t)r * pitch, (long long)nd * 4);
     uint32_t* out = rowseg + (size_t)f * ns * rs_rows + r;
@@ -580,8 +583,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(16))) void k_ii
             const uint32_t inc = carry + wave_excl_scan(x, tot) + x;
             carry += tot;
             // dword d ends at column 4 d + 3: the last one below cs_k when
-            // 4 (d + 1) = 480 k - 144, i.e. d + 37 = 120 k
-            if (d < nd && (d + 37) % (hw::ST / 4) == 0) out[(size_t)((d + 37) / (hw::ST / 4)) * rs_rows] = inc;
+            // 4 (d + 1) = ST k - HALO, i.e. d + 1 + HALO / 4 = (ST / 4) k
+            constexpr int DO = 1 + HALO / 4;
+            if (d < nd && (d + DO) % (ST / 4) == 0) out[(size_t)((d + DO) / (ST / 4)) * rs_rows] = inc;
         }
     }
 }
@@ -589,10 +593,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(16))) void k_ii
 hipError_t launch_rowseg(const uint8_t* frames, int pitch, long long fstride, int nframes, const FrameParams& P,
                          const LaunchPlan& plan, uint32_t* rowseg, hipStream_t s)
 {
-    if (!plan.iiw) return hipSuccess;
-    if (plan.hw_nstrips > 1)
-        k_ii_rowseg<<<dim3((P.H + 3) / 4, nframes), 256, 0, s>>>(frames, pitch, fstride, P.H, plan.hw_nstrips,
-                                                                  plan.rs_rows, rowseg);
+    if (!plan.iiw || plan.rs_nstrips < 2) return hipSuccess;
+    const dim3 g((P.H + 3) / 4, nframes);
+    if (plan.iiw == 2)
+        k_ii_rowseg<128, 16><<<g, 256, 0, s>>>(frames, pitch, fstride, P.H, plan.rs_nstrips, plan.rs_rows, rowseg);
+    else
+        k_ii_rowseg<hw::ST, hw::H><<<g, 256, 0, s>>>(frames, pitch, fstride, P.H, plan.rs_nstrips, plan.rs_rows,
+                                                     rowseg);
     return hipGetLastError();
 }
 
@@ -708,13 +715,17 @@ void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, 
     }
     plan.hess_start[kMaxOct] = hb;
     plan.nms_start[kMaxOct] = nb;
-    // the integral image from k_hess_w (SURFHIP_II_FUSE=0 disables): octave
-    // 0 on k_hess_p0 and octaves 1-3 on k_hess_w; octaves past 3 (k_hessian)
-    // then read the integral k_hess_w wrote, after it on the same stream
+    // the integral image from k_hess_w (SURFHIP_II_FUSE=0 disables, =2 moves
+    // it to k_hess_p0's producer): octave 0 on k_hess_p0 and octaves 1-3 on
+    // k_hess_w; octaves past 3 (k_hessian) then read the integral written,
+    // after them on the same stream
     {
         const char* fe = getenv("SURFHIP_II_FUSE");
-        plan.iiw = plan.hw_n >= 2 && plan.p0 != 0 && !plan.t0 && !(fe && atoi(fe) == 0);
+        const int fv = fe ? atoi(fe) : 1;
+        const bool on = plan.hw_n >= 2 && plan.p0 != 0 && !plan.t0 && fv != 0;
+        plan.iiw = !on ? 0 : (fv == 2 && plan.p0 == 93) ? 2 : 1;
         plan.rs_rows = 4 * plan.hw_nblk;
+        plan.rs_nstrips = plan.iiw == 2 ? plan.q0_strips : plan.hw_nstrips;
     }
 }
 
@@ -739,7 +750,7 @@ std::string hessian_plan_text(const LaunchPlan& plan, const FrameParams& P)
     if (plan.hw_n > 0) add("k_hess_w", 1, plan.hw_n);
     // (the row-sum pass runs before the stage: beside the previous batch's
     // NMS when pipelined, like the integral passes it replaces)
-    if (plan.iiw) t += ", writing the integral image";
+    if (plan.iiw) t += plan.iiw == 2 ? ", writing the integral image (k_hess_p0)" : ", writing the integral image";
     if (plan.hess_start[kMaxOct] > 0) {
         int lo = -1, hi = -1;
         for (int o = 0; o < P.noct; o++)
@@ -876,7 +887,7 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
         if (plan.hw_n > 0) {
             const dim3 g(nf8 * plan.hw_nstrips);
             const OctaveParams& q3 = h_oct[plan.hw_n >= 3 ? 3 : 2];
-            const bool wr = plan.iiw && ii_out && rowseg;
+            const bool wr = plan.iiw == 1 && ii_out && rowseg;
 #define HW_LAUNCH(NO, IIW)                                                                                       \
     k_hess_w<NO, IIW><<<g, hw::THREADS, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[1], h_oct[2], q3,          \
                                                 plan.hw_nstrips, nframes, plan.hw_nblk, rowseg, ii_out, plan.rs_rows)
@@ -899,10 +910,14 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
         } else {
             const dim3 gp(nf8 * plan.q0_strips);
             const int pb = plan.p0 / 10, pg = plan.p0 % 10;      // interval, consumer waves
+            // (iiw 2, only with the default 93: this launch writes the integral)
+            const bool wr0 = plan.iiw == 2 && ii_out && rowseg;
 #define P0_CASE(BB, GG)                                                                                          \
-    else if (pb == BB && pg == GG) k_hess_p0<BB, GG, 1><<<gp, 64 * (1 + GG), 0, s>>>(frames, pitch, fstride, resp, P, \
-                                                                                    h_oct[0], plan.q0_strips, nframes);
-            if (false) {}
+    else if (pb == BB && pg == GG) k_hess_p0<BB, GG, 1, false><<<gp, 64 * (1 + GG), 0, s>>>(                       \
+        frames, pitch, fstride, resp, P, h_oct[0], plan.q0_strips, nframes, nullptr, nullptr, 0);
+            if (wr0 && pb == 9 && pg == 3)
+                k_hess_p0<9, 3, 1, true><<<gp, 64 * 4, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
+                                                               plan.q0_strips, nframes, rowseg, ii_out, plan.rs_rows);
             P0_CASE(9, 5) P0_CASE(9, 4) P0_CASE(9, 3) P0_CASE(9, 2) P0_CASE(9, 1) P0_CASE(3, 2) P0_CASE(3, 3)
 #undef P0_CASE
             else if (plan.q0)

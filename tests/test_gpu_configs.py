@@ -353,21 +353,26 @@ def test_run_hessian_without_integral(surf):
     det.close()
 
 
-@pytest.mark.parametrize("w,h", [(960, 130), (1001, 97), (1002, 64), (1003, 71), (481, 50), (1920, 1080)])
-def test_fused_integral_from_hessian(surf, orc, w, h):
-    """plan.iiw: k_hess_w's producers write the integral image (their strip
-    integral plus k_ii_rowseg's row sums left of the strip), no separate
-    integral pass.  Bit-exact against the oracle for widths on and off the
-    480-column strip grid and every W % 4 (the lane holding column W stores
-    only columns <= W; the pad columns stay 0), through detect_batch and
-    through the pipelined entry point (row sums prefetched by the previous
-    call)."""
+@pytest.mark.parametrize("fuse", ["1", "2"])
+@pytest.mark.parametrize("w,h", [(960, 130), (1001, 97), (1002, 64), (1003, 71), (481, 50), (1025, 40),
+                                 (1920, 1080)])
+def test_fused_integral_from_hessian(surf, orc, monkeypatch, fuse, w, h):
+    """plan.iiw: a u8 Hessian kernel's producers write the integral image
+    (their strip integral plus k_ii_rowseg's row sums left of the strip), no
+    separate integral pass -- k_hess_w (480-column strips, SURFHIP_II_FUSE=1)
+    or k_hess_p0 (128-column strips, =2).  Bit-exact against the oracle for
+    widths on and off both strip grids and every W % 4 (the lane holding
+    column W stores only columns <= W; the pad columns stay 0), through
+    detect_batch and through the pipelined entry point (row sums prefetched
+    by the previous call)."""
+    monkeypatch.setenv("SURFHIP_II_FUSE", fuse)
     n = 3
     frames = surf.synth_frames(n, w, h, first=900)
     pitch = frames.shape[2]
     param = surf.make_param(4, 4.0, upright=True)
     det = surf.Detector(param, w, h, max_batch=n, max_pts=4096)
     assert "writing the integral image" in det.hessian_kernels()
+    assert ("(k_hess_p0)" in det.hessian_kernels()) == (fuse == "2")
     fb = [surf.DeviceBuffer(frames.nbytes) for _ in range(2)]
     fb[0].upload(frames)
     fb[1].upload(frames[::-1].copy())
