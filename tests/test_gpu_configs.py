@@ -397,6 +397,35 @@ def test_fused_integral_from_hessian(surf, orc, monkeypatch, fuse, w, h):
     det.close()
 
 
+@pytest.mark.parametrize("fuse", ["1", "2"])
+def test_fused_integral_batch256(surf, orc, monkeypatch, fuse):
+    """The fused integral of a full 256 x 1080p batch, frames spread over the
+    batch, bit-exact against the oracle.  (k_hess_p0's integral stores with
+    the row offset as the scalar offset left wrong values in rows 11-90 of
+    every frame from 16 on, tools/ii_batch_check.py; 3-frame batches did not
+    show it.)"""
+    monkeypatch.setenv("SURFHIP_II_FUSE", fuse)
+    n, w, h = 256, 1920, 1080
+    frames = surf.synth_frames(n, w, h)
+    pitch = frames.shape[2]
+    param = surf.make_param(4, 4.0, upright=True)
+    det = surf.Detector(param, w, h, max_batch=n, max_pts=8192)
+    fb = surf.DeviceBuffer(frames.nbytes)
+    fb.upload(frames)
+    pb = surf.DeviceBuffer(48 * n * 8192)
+    cb = surf.DeviceBuffer(4 * n)
+    det.detect_batch(fb.ptr, n, pitch, h * pitch, pb.ptr, None, cb.ptr)
+    surf.synchronize()
+    ii, iis, _, _ = det.workspace()
+    ip = surf.align_up(w + 1, 128)
+    for f in [0, 1, 7, 8, 14, 15] + list(range(115, 136)) + [240, 255]:
+        got = surf.download_ptr(ii + 4 * f * iis, np.int32, (h + 1) * ip).reshape(h + 1, ip)
+        ref = orc.integral(frames[f], w, h)
+        bad = np.argwhere(got != ref)
+        assert len(bad) == 0, (fuse, f, len(bad), bad[:4].tolist())
+    det.close()
+
+
 def test_fused_integral_switch(surf, monkeypatch):
     """SURFHIP_II_FUSE=0 keeps the separate integral passes (A/B); the gather
     plan (few frames) never fuses; a 5-octave plan does (octave 4's k_hessian
