@@ -240,6 +240,12 @@ def download_ptr(ptr: int, dtype, count: int) -> np.ndarray:
     return out
 
 
+def upload_ptr(ptr: int, arr: np.ndarray) -> None:
+    a = np.ascontiguousarray(arr)
+    if a.nbytes:
+        check(_lib.surfhip_memcpy(ptr, a.ctypes.data, a.nbytes, H2D), "upload")
+
+
 # ---------------------------------------------------------------- detector
 
 def make_param(noctaves=4, thresh=0.2, doubled=False, init_mask_size=9, sampling_step=2,

@@ -426,6 +426,70 @@ def test_fused_integral_batch256(surf, orc, monkeypatch, fuse):
     det.close()
 
 
+def _fused_ii_with_guard(surf, frames, w, h, param, monkeypatch, fuse):
+    """detect_batch of `frames` on a detector with one spare frame slot whose
+    integral region holds a canary; returns (integral of every frame, the
+    guard region after the last one, the canary)."""
+    monkeypatch.setenv("SURFHIP_II_FUSE", fuse)
+    n = len(frames)
+    pitch = frames.shape[2]
+    det = surf.Detector(param, w, h, max_batch=n + 1, max_pts=4096)
+    assert "writing the integral image" in det.hessian_kernels()
+    ii, iis, _, _ = det.workspace()
+    canary = np.full(iis, 0x5A5A5A5A, np.uint32)
+    surf.upload_ptr(ii + 4 * n * iis, canary)
+    fb = surf.DeviceBuffer(frames.nbytes)
+    fb.upload(frames)
+    pb = surf.DeviceBuffer(48 * n * 4096)
+    cb = surf.DeviceBuffer(4 * n)
+    det.detect_batch(fb.ptr, n, pitch, h * pitch, pb.ptr, None, cb.ptr)
+    surf.synchronize()
+    got = surf.download_ptr(ii, np.int32, (n + 1) * iis).reshape(n + 1, iis)
+    det.close()
+    return got[:n], got[n].view(np.uint32), canary
+
+
+@pytest.mark.parametrize("fuse", ["1", "2"])
+@pytest.mark.parametrize("w,h", [(640, 240), (1920, 1040)])
+def test_fused_integral_rows_past_frame_canary(surf, orc, monkeypatch, fuse, w, h):
+    """VERDICT r05 item 1.  k_hess_w's producers walk 4 hw_nblk integral rows
+    (hw_nblk: whole 20-block ring iterations), k_hess_p0's from row -16: for H
+    = 80 m that is 79 rows past the frame's H + 1 -- the most any height gives.
+    Frames' integrals are packed back to back (ii_stride = (H + 1) ip), so a
+    store of those rows that the range check let through would land in the
+    next frame's first rows or, after the last frame, in the spare slot's
+    canary.  Every frame bit-exact, the canary intact."""
+    hw_nblk = ((h // 4 + 1 + 19) // 20) * 20
+    assert 4 * hw_nblk - (h + 1) == 79
+    n = 16
+    frames = surf.synth_frames(n, w, h, first=4000)
+    param = surf.make_param(4, 4.0, upright=True)
+    got, guard, canary = _fused_ii_with_guard(surf, frames, w, h, param, monkeypatch, fuse)
+    ip = surf.align_up(w + 1, 128)
+    for f in range(n):
+        ref = orc.integral(frames[f], w, h)
+        bad = np.argwhere(got[f][: (h + 1) * ip].reshape(h + 1, ip) != ref)
+        assert len(bad) == 0, (fuse, f, len(bad), bad[:4].tolist())
+    assert np.array_equal(guard, canary), (fuse, int((guard != canary).sum()))
+
+
+@pytest.mark.parametrize("fuse", ["1", "2"])
+def test_fused_integral_saturated_4k(surf, orc, monkeypatch, fuse):
+    """the all-255 3840 x 2160 frame through the fused
+    writers (k_hess_w's / k_hess_p0's producers, 5 octaves as config #5): the
+    image's integral tops out at 2,115,072,000 (< 2^31) and the producers'
+    uint32 carries must reach it exactly; canary after the frame intact."""
+    w, h = 3840, 2160
+    frames = np.full((1, h, surf.align_up(w, 128)), 255, np.uint8)
+    param = surf.make_param(5, 4.0, upright=True)
+    got, guard, canary = _fused_ii_with_guard(surf, frames, w, h, param, monkeypatch, fuse)
+    ip = surf.align_up(w + 1, 128)
+    ii0 = got[0][: (h + 1) * ip].reshape(h + 1, ip)
+    assert ii0[h, w] == 255 * w * h
+    np.testing.assert_array_equal(ii0, orc.integral(frames[0], w, h))
+    assert np.array_equal(guard, canary)
+
+
 def test_fused_integral_switch(surf, monkeypatch):
     """SURFHIP_II_FUSE=0 keeps the separate integral passes (A/B); the gather
     plan (few frames) never fuses; a 5-octave plan does (octave 4's k_hessian
