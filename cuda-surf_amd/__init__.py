@@ -134,6 +134,8 @@ _sigs = {
     "surfhip_ingest_pending": (_i, [_vp, C.POINTER(_i)]),
     "surfhip_dump_append": (_i, [C.c_char_p, _vp, _sz, _i, _i, C.POINTER(SurfParam), C.c_longlong]),
     "surfhip_build_info": (C.c_char_p, []),
+    "surfhip_stream_run": (_i, [_i, _vp, _vp, _sz, _vp]),
+    "surfhip_stream_bytes": (_sz, [_i, _sz]),
 }
 for _name, (_res, _args) in _sigs.items():
     _f = getattr(_lib, _name)
@@ -238,6 +240,17 @@ def download_ptr(ptr: int, dtype, count: int) -> np.ndarray:
     if out.nbytes:
         check(_lib.surfhip_memcpy(out.ctypes.data, ptr, out.nbytes, D2H), "download")
     return out
+
+
+STREAM_MODES = {"copy": 0, "read": 1, "write": 2}
+
+
+def stream_run(mode: str, src: int | None, dst: int | None, nbytes: int, stream=None) -> int:
+    """One launch of the HBM stream-rate kernel (surfhip_stream_run); returns
+    the HBM bytes it moves (copy: read + write)."""
+    m = STREAM_MODES[mode]
+    check(_lib.surfhip_stream_run(m, src, dst, nbytes, stream), f"stream_run({mode})")
+    return int(_lib.surfhip_stream_bytes(m, nbytes))
 
 
 def upload_ptr(ptr: int, arr: np.ndarray) -> None:

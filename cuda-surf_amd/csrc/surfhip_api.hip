@@ -1244,6 +1244,21 @@ int surfhip_dump_append(const char* path, const void* h_slab, size_t bytes, int 
     return ok ? SURFHIP_OK : SURFHIP_ERR_INVALID;
 }
 
+int surfhip_stream_run(int mode, const void* src, void* dst, size_t bytes, void* stream)
+{
+    if (mode < 0 || mode > 2 || bytes % 16 != 0 || ((uintptr_t)src & 15) || ((uintptr_t)dst & 15) ||
+        (mode != 2 && !src) || (mode != 1 && !dst))
+        return SURFHIP_ERR_INVALID;
+    if (bytes == 0) return SURFHIP_OK;
+    int dev = 0, ncu = 0;
+    HIPCHK(hipGetDevice(&dev));
+    HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    HIPCHK(surfhip::launch_stream(mode, src, dst, bytes, ncu, (hipStream_t)stream));
+    return SURFHIP_OK;
+}
+
+size_t surfhip_stream_bytes(int mode, size_t bytes) { return mode == 0 ? 2 * bytes : mode == 1 || mode == 2 ? bytes : 0; }
+
 const char* surfhip_build_info(void)
 {
     return "libsurfhip gfx950 (" __DATE__ " " __TIME__ ")";

@@ -177,6 +177,8 @@ hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_poin
                            float* desc, int* queue, hipStream_t s, bool beside, int cus);
 // Doubled-image input (surfhip_double.hip): frames (W x H) -> D ((2W-2) x
 // (2H-2) u8, row pitch dpitch, a multiple of 4).
+// HBM stream-rate kernels (surfhip_stream.hip): mode 0 copy, 1 read, 2 write
+hipError_t launch_stream(int mode, const void* src, void* dst, size_t bytes, int ncu, hipStream_t s);
 hipError_t launch_double(const uint8_t* frames, int pitch, long long fstride, int nframes, int W, int H,
                          uint8_t* dst, int dpitch, long long dstride, hipStream_t s);
 // Descriptor matching (surfhip_match.hip): scratch = match_scratch_bytes().

@@ -318,6 +318,19 @@ typedef struct surfhip_dump_header {
 int surfhip_dump_append(const char* path, const void* h_slab, size_t bytes, int width, int height,
                         const surfhip_param* param, long long first_frame);
 
+/* Measured HBM stream rates (SURVEY 8d "also report measured peak from an
+ * in-repo stream-copy kernel"; no reference counterpart).  One launch of a
+ * 16-B-per-lane streaming kernel over `bytes` (a multiple of 16, src and dst
+ * 16-B aligned) on `stream`, all 256 CUs, grid-stride:
+ *   mode 0 copy  src -> dst  (moves 2 x bytes: read + write)
+ *   mode 1 read  src only    (dst written only if a running XOR hits a
+ *                             64-bit magic: never, for practical data)
+ *   mode 2 write dst only    (writes bytes)
+ * The caller times launches with events; surfhip_stream_bytes gives the HBM
+ * bytes one launch of a mode moves. */
+int surfhip_stream_run(int mode, const void* src, void* dst, size_t bytes, void* stream);
+size_t surfhip_stream_bytes(int mode, size_t bytes);
+
 /* Library build identification (for the loaded-.so audit). */
 const char* surfhip_build_info(void);
 

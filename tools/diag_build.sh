@@ -6,7 +6,7 @@
 set -eu
 cd "$(dirname "$0")/../cuda-surf_amd"
 H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -I../include -Icsrc -mllvm -amdgpu-atomic-optimizer-strategy=None"
-make -s build/surfhip_api.o build/surfhip_match.o build/surfhip_double.o
+make -s build/surfhip_api.o build/surfhip_match.o build/surfhip_double.o build/surfhip_stream.o
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   D=""; IFS=, read -ra FL <<< "$flags"; for f in "${FL[@]}"; do [ -n "$f" ] && D="$D -D$f"; done
@@ -16,7 +16,7 @@ done
 wait
 for spec in "$@"; do
   name=${spec%%:*}
-  $H -shared -fPIC -o diag/$name/libsurfhip.so diag/$name/k.o build/surfhip_api.o build/surfhip_match.o build/surfhip_double.o
+  $H -shared -fPIC -o diag/$name/libsurfhip.so diag/$name/k.o build/surfhip_api.o build/surfhip_match.o build/surfhip_double.o build/surfhip_stream.o
   rm -f diag/$name/k.o
 done
 echo built "$@"
