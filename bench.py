@@ -605,6 +605,10 @@ def run_rank(args):
                          # the copy rate (read + write, the stage's mix)
                          "peak_measured": peaks,
                          "frac_measured": (round(achieved / peaks["copy_GBps"], 4) if peaks else None),
+                         # the stage's algorithmic reads and writes each at
+                         # the measured read / write rate: the time HBM needs
+                         # for this byte mix, and the stage's fraction of it
+                         **mix_floor(peaks, hb, W, H, B, "writing the integral image" in kern, hess_ms),
                          # the same bytes over the sum of the stage kernels'
                          # rocprof average durations in the committed trace
                          "launch_ms_profile": round(hp["stage_ms"], 4) if hp else None,
@@ -632,8 +636,16 @@ def run_rank(args):
                                                  "the batch's own integral beside them" if args.no_pipeline else
                                                  "the next batch's integral beside the NMS stage instead")
                                               if hess_instep else "serial"),
-                         "launch_ms_serial": round(hess_serial_ms, 4)},
+                         "launch_ms_serial": round(hess_serial_ms, 4),
+                         #  the integral the stage writes also
+                         # needs k_ii_rowseg's row sums (1,296 of 1,920 columns
+                         # read), which run outside the bracket beside the
+                         # previous describe: their serial time, and the
+                         # fraction with it added to the stage
+                         **(rowseg_terms(stage_acc, nprof, hb, hess_ms)
+                            if "writing the integral image" in kern else {})},
             "gen_s": round(gen_s, 2),
+            "device": _device_info(surf, dev.index),
         }
         if exchanged is not None:
             result["exchange"] = exchanged
@@ -670,6 +682,37 @@ class _StdoutToStderr:
         os.dup2(self.saved, 1)
         os.close(self.saved)
         return False
+
+
+def mix_floor(peaks, hb, W, H, B, fused, hess_ms):
+    """HBM time of the Hessian stage's algorithmic bytes at the measured
+    stream rates: reads (the u8 frames when the stage writes the integral
+    image, else the integral image) at the read rate, writes (responses, and
+    the integral image when fused) at the write rate."""
+    if not peaks:
+        return {"floor_ms_measured": None, "frac_floor": None}
+    rd = (W * H if fused else (W + 1) * (H + 1) * 4) * B
+    wr = hb - rd
+    floor = rd / (peaks["read_GBps"] * 1e6) + wr / (peaks["write_GBps"] * 1e6)
+    return {"floor_bytes": {"read": rd, "write": wr}, "floor_ms_measured": round(floor, 4),
+            "frac_floor": round(floor / hess_ms, 4)}
+
+
+def rowseg_terms(stage_acc, nprof, hb, hess_ms):
+    rs = stage_acc.get("integral")
+    if not rs:
+        return {"rowseg_ms_serial": None, "frac_with_rowseg": None}
+    rs_ms = rs / nprof
+    return {"rowseg_ms_serial": round(rs_ms, 4),
+            "frac_with_rowseg": round(hb / ((hess_ms + rs_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def _device_info(surf, index):
+    try:
+        name, cus = surf.device_name(index)
+        return {"name": name, "cus": cus}
+    except Exception as e:                                  # informational only
+        return {"error": str(e)}
 
 
 def stream_peaks(surf, torch, dev, stream, nbytes=2 << 30, reps=10):

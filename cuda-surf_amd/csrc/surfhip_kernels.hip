@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <cstdlib>
 #include <mutex>
@@ -1877,6 +1878,7 @@ constexpr int kRankLds = 16384;
 // workgroup.  (One lane per candidate walked all ~3,000 keys of a 1080p
 // frame on one wave per SIMD of a dozen CUs: 27-29 us per frame.)
 constexpr int kRankT = 16;                      // lanes per candidate
+constexpr int kRankMaxWgs = 256;                // workgroups per frame at most
 __global__ __launch_bounds__(256) void k_sort_rank(const surfhip_point* __restrict__ cand,
                                                    const uint32_t* __restrict__ keys,
                                                    const int* __restrict__ cand_count,
@@ -1918,33 +1920,38 @@ __global__ __launch_bounds__(256) void k_sort_rank(const surfhip_point* __restri
         if (cand_count[f] > valid) atomicOr(status, 1);
     }
     const int part = (int)(threadIdx.x & (kRankT - 1));
-    const int i = r * CPW + (int)(threadIdx.x / kRankT);
-    const uint32_t ki = (i < cnt) ? (lds ? sk[i] : fk[i]) : kNoKey;
-    int rank = 0;
-    if (ki != kNoKey) {
-        if (lds) {
-            int j = part;
-            for (; j + 7 * kRankT < cnt; j += 8 * kRankT) {
-                uint32_t q[8];
+    // candidate groups r, r + wgs, ...: a dense frame (cnt up to the cap)
+    // reuses the keys staged in LDS for several groups instead of restaging
+    // them in cnt / 16 workgroups (16x the key loads)
+    for (int g = r; g * CPW < cnt; g += wgs_per_frame) {
+        const int i = g * CPW + (int)(threadIdx.x / kRankT);
+        const uint32_t ki = (i < cnt) ? (lds ? sk[i] : fk[i]) : kNoKey;
+        int rank = 0;
+        if (ki != kNoKey) {
+            if (lds) {
+                int j = part;
+                for (; j + 7 * kRankT < cnt; j += 8 * kRankT) {
+                    uint32_t q[8];
 #pragma unroll
-                for (int u = 0; u < 8; u++) q[u] = sk[j + u * kRankT];
+                    for (int u = 0; u < 8; u++) q[u] = sk[j + u * kRankT];
 #pragma unroll
-                for (int u = 0; u < 8; u++) rank += q[u] < ki;
+                    for (int u = 0; u < 8; u++) rank += q[u] < ki;
+                }
+                for (; j < cnt; j += kRankT) rank += sk[j] < ki;
+            } else {
+                for (int j = part; j < cnt; j += kRankT) rank += fk[j] < ki;
             }
-            for (; j < cnt; j += kRankT) rank += sk[j] < ki;
-        } else {
-            for (int j = part; j < cnt; j += kRankT) rank += fk[j] < ki;
         }
-    }
-    // the 16 partial counts of a candidate: DPP row shifts (16-lane rows)
-    rank += __builtin_amdgcn_update_dpp(0, rank, 0x111, 0xf, 0xf, false);      // row_shr:1
-    rank += __builtin_amdgcn_update_dpp(0, rank, 0x112, 0xf, 0xf, false);      // row_shr:2
-    rank += __builtin_amdgcn_update_dpp(0, rank, 0x114, 0xf, 0xf, false);      // row_shr:4
-    rank += __builtin_amdgcn_update_dpp(0, rank, 0x118, 0xf, 0xf, false);      // row_shr:8
-    // lane 15 of each row holds the row's sum
-    if (part == kRankT - 1 && ki != kNoKey && rank < keep) {
-        out[(size_t)f * max_pts + rank] = cand[(size_t)f * cap + i];
-        order[(size_t)f * max_pts + rank] = rank;
+        // the 16 partial counts of a candidate: DPP row shifts (16-lane rows)
+        rank += __builtin_amdgcn_update_dpp(0, rank, 0x111, 0xf, 0xf, false);      // row_shr:1
+        rank += __builtin_amdgcn_update_dpp(0, rank, 0x112, 0xf, 0xf, false);      // row_shr:2
+        rank += __builtin_amdgcn_update_dpp(0, rank, 0x114, 0xf, 0xf, false);      // row_shr:4
+        rank += __builtin_amdgcn_update_dpp(0, rank, 0x118, 0xf, 0xf, false);      // row_shr:8
+        // lane 15 of each row holds the row's sum
+        if (part == kRankT - 1 && ki != kNoKey && rank < keep) {
+            out[(size_t)f * max_pts + rank] = cand[(size_t)f * cap + i];
+            order[(size_t)f * max_pts + rank] = rank;
+        }
     }
 }
 
@@ -1980,7 +1987,10 @@ hipError_t launch_sort(const surfhip_point* cand, const uint32_t* keys, uint64_t
                        hipStream_t s)
 {
     if (nframes <= kRankBatch && getenv("SURFHIP_SORT_BITONIC") == nullptr) {
-        const int per = (cap + 256 / kRankT - 1) / (256 / kRankT);
+        // workgroups per frame: one per 16 candidates up to 256 (~3,000
+        // candidates of a 1080p frame: 188), beyond that each takes several
+        // groups of 16 with the keys it staged once
+        const int per = std::min((cap + 256 / kRankT - 1) / (256 / kRankT), kRankMaxWgs);
         k_sort_rank<<<nframes * per, 256, 0, s>>>(cand, keys, cand_count, soff, items_per_frame, cap, per, out,
                                                   max_pts, out_count, order, status);
     } else {
@@ -3266,7 +3276,9 @@ __global__ __launch_bounds__(256) void k_worklist(const surfhip_point* __restric
     // max_pts-sized grid would find nothing to do).  Entry = two float4 of
     // the keypoint's window geometry, the describe kernel's per-keypoint
     // set-up moved here (surfd.cu:1581-1596, the upright branch of describe):
-    //   {dx, dy, spacing, f}  {ix, iy, step | hs << 8 | iradius << 20, f * max_pts + kp}
+    //   {dx, dy, spacing, f}  {ix, iy, step | hs << 10 | iradius << 22, f * max_pts + kp}
+    // (10 / 12 / 10 bits: launch_describe takes this path only when the
+    // largest window of the detector's octaves fits, worklist_fits)
     const int f = blockIdx.y, n = counts[f], o = offsets[f];
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const int idx = f * max_pts + order[(size_t)f * max_pts + i];
@@ -3280,9 +3292,25 @@ __global__ __launch_bounds__(256) void k_worklist(const surfhip_point* __restric
         const int iradius = f2i_rn(((spacing * (float)(P.wsz + 1)) * 0.5f) / (float)step);
         work[2 * (size_t)(o + i)] = make_float4(at.x - (float)ix, at.y - (float)iy, spacing, __int_as_float(f));
         work[2 * (size_t)(o + i) + 1] =
-            make_float4(__int_as_float(ix), __int_as_float(iy), __int_as_float(step | (hs << 8) | (iradius << 20)),
+            make_float4(__int_as_float(ix), __int_as_float(iy), __int_as_float(step | (hs << 10) | (iradius << 22)),
                         __int_as_float(idx));
     }
+}
+
+// Whether k_worklist's packed fields hold every keypoint window of this
+// detector: the largest keypoint scale is makePoint's 1.2 ns
+// divisor (surfd.cu:1001-1022) at the top octave with s + off <= max_scale -
+// 1 + 1.5 (the fit's limits); describe uses 1.65 x (3.3 x doubled) of it
+// (surfd.cu:1581-1592); step = rn(S / 2) < 2^10, hs = rz(S) < 2^12, iradius
+// = rn(spacing (wsz + 1) / 2 / step) < 2^10.
+static bool worklist_fits(const FrameParams& P)
+{
+    const float oct = (float)(1 << (P.noct - 1));
+    const float ns = ((float)P.init_lobe + (oct - 1.f) * (float)P.max_scale + ((float)P.max_scale + 0.5f) * 2.f * oct) / 3.f;
+    const float S = (P.doubled ? 3.3f : 1.65f) * 1.2f * ns * P.divisor;
+    const float step = std::max(std::floor(S * 0.5f + 0.5f), 1.f);
+    const float iradius = S * (float)P.mag * (float)(P.wsz + 1) * 0.5f / step + 1.f;
+    return S * 0.5f + 1.f < 1024.f && S + 1.f < 4096.f && iradius < 1024.f;
 }
 
 hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
@@ -3306,7 +3334,7 @@ hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_poin
     // one 1080p frame's describe 0.032 -> 0.030 ms)
     const char* ur = getenv("SURFHIP_DESC_UR");
     const bool use_u2 = ur ? atoi(ur) == 0 : nframes > kGatherBatch;
-    if (P.upright && P.wsz == 4 && use_u2) {
+    if (P.upright && P.wsz == 4 && use_u2 && worklist_fits(P)) {
         k_worklist<<<dim3(std::min(8, (max_pts + 255) / 256), nframes), 256, 0, s>>>(pts, max_pts, counts, offsets,
                                                                                       order, work, P);
         // (diagnostic: SURFHIP_U2_LDSPAD bytes of unused dynamic LDS per workgroup)

@@ -3,13 +3,9 @@
 // stream-copy kernel").  No reference counterpart: the
 // reference never measures bandwidth.
 //
-// One 16-B load and/or store per lane per step, 4 steps unrolled so each
-// lane keeps 4 loads in flight, grid-stride over the buffer; the grid is 8
-// workgroups of 256 per CU (one launch fills the chip several times over).
-// Copy and read use non-temporal loads (each byte is read once), stores
-// the default policy (measured faster for the plane / integral writers,
-// DESIGN §4).  The read kernel keeps its sums live by a store that never
-// happens for real data (an XOR equal to a 64-bit magic).
+// 16-B accesses per lane, several in flight.  The read kernel keeps its
+// sums live by a store that never happens for real data (an XOR equal to a
+// 64-bit magic).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -19,34 +15,46 @@ namespace surfhip {
 
 namespace {
 
-constexpr int kStreamUnroll = 4;
 typedef uint32_t u4 __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(256) void k_stream_copy(const u4* __restrict__ src, u4* __restrict__ dst, size_t n)
+// The forms below are the fastest of tools/ubench/stream_sweep.hip's sweep
+// (profiles/r06b/stream_sweep.txt, 2-GiB buffers): copy as contiguous
+// per-workgroup chunks with non-temporal loads and stores, 8 workgroups per
+// CU (5.36 TB/s read + write; grid-stride forms 4.1-4.96); read grid-stride
+// with 8 non-temporal 16-B loads in flight per lane, 32 workgroups per CU
+// (6.24 TB/s); write grid-stride, 4 default-policy 16-B stores per lane, 8
+// workgroups per CU (4.64 TB/s; nt stores 4.42-4.45).
+constexpr int kCopyU = 4;
+
+__global__ __launch_bounds__(256) void k_stream_copy(const u4* __restrict__ src, u4* __restrict__ dst, size_t n,
+                                                     size_t per_wg)
 {
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + (kStreamUnroll - 1) * stride < n; i += kStreamUnroll * stride) {
-        u4 v[kStreamUnroll];
+    const size_t b0 = (size_t)blockIdx.x * per_wg;
+    const size_t e = b0 + per_wg < n ? b0 + per_wg : n;
+    for (size_t i = b0 + threadIdx.x; i < e; i += kCopyU * 256) {
+        u4 v[kCopyU];
 #pragma unroll
-        for (int k = 0; k < kStreamUnroll; k++) v[k] = __builtin_nontemporal_load(src + i + k * stride);
+        for (int k = 0; k < kCopyU; k++)
+            v[k] = i + k * 256 < e ? __builtin_nontemporal_load(src + i + k * 256) : u4{0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int k = 0; k < kStreamUnroll; k++) dst[i + k * stride] = v[k];
+        for (int k = 0; k < kCopyU; k++)
+            if (i + k * 256 < e) __builtin_nontemporal_store(v[k], dst + i + k * 256);
     }
-    for (; i < n; i += stride) dst[i] = __builtin_nontemporal_load(src + i);
 }
+
+constexpr int kReadU = 8;
 
 __global__ __launch_bounds__(256) void k_stream_read(const u4* __restrict__ src, u4* __restrict__ dst, size_t n)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t a = 0u, b = 0u;
-    for (; i + (kStreamUnroll - 1) * stride < n; i += kStreamUnroll * stride) {
-        u4 v[kStreamUnroll];
+    for (; i + (kReadU - 1) * stride < n; i += kReadU * stride) {
+        u4 v[kReadU];
 #pragma unroll
-        for (int k = 0; k < kStreamUnroll; k++) v[k] = __builtin_nontemporal_load(src + i + k * stride);
+        for (int k = 0; k < kReadU; k++) v[k] = __builtin_nontemporal_load(src + i + k * stride);
 #pragma unroll
-        for (int k = 0; k < kStreamUnroll; k++) {
+        for (int k = 0; k < kReadU; k++) {
             a ^= v[k].x ^ v[k].z;
             b ^= v[k].y ^ v[k].w;
         }
@@ -59,11 +67,17 @@ __global__ __launch_bounds__(256) void k_stream_read(const u4* __restrict__ src,
     if (a == 0x9E3779B9u && b == 0x7F4A7C15u) dst[0] = u4{a, b, a, b};
 }
 
+constexpr int kWriteU = 4;
+
 __global__ __launch_bounds__(256) void k_stream_write(u4* __restrict__ dst, size_t n)
 {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const u4 v = {(uint32_t)i, 1u, 2u, 3u};
+    for (; i + (kWriteU - 1) * stride < n; i += kWriteU * stride) {
+#pragma unroll
+        for (int k = 0; k < kWriteU; k++) dst[i + k * stride] = v;
+    }
     for (; i < n; i += stride) dst[i] = v;
 }
 
@@ -72,13 +86,15 @@ __global__ __launch_bounds__(256) void k_stream_write(u4* __restrict__ dst, size
 hipError_t launch_stream(int mode, const void* src, void* dst, size_t bytes, int ncu, hipStream_t s)
 {
     const size_t n = bytes / 16;
-    const dim3 grid((unsigned)(8 * (ncu > 0 ? ncu : 256)));
-    if (mode == 0)
-        k_stream_copy<<<grid, 256, 0, s>>>((const u4*)src, (u4*)dst, n);
-    else if (mode == 1)
-        k_stream_read<<<grid, 256, 0, s>>>((const u4*)src, (u4*)dst, n);
-    else
-        k_stream_write<<<grid, 256, 0, s>>>((u4*)dst, n);
+    if (ncu <= 0) ncu = 256;
+    if (mode == 0) {
+        const unsigned g = (unsigned)(8 * ncu);
+        k_stream_copy<<<g, 256, 0, s>>>((const u4*)src, (u4*)dst, n, (n + g - 1) / g);
+    } else if (mode == 1) {
+        k_stream_read<<<(unsigned)(32 * ncu), 256, 0, s>>>((const u4*)src, (u4*)dst, n);
+    } else {
+        k_stream_write<<<(unsigned)(8 * ncu), 256, 0, s>>>((u4*)dst, n);
+    }
     return hipGetLastError();
 }
 
