@@ -6,6 +6,9 @@ into the committed summaries under profiles/:
   profiles/<tag>_pmc.csv            per-kernel mean FETCH_SIZE / WRITE_SIZE (KB)
   profiles/<tag>_bench.json         the bench line of the profiled run
   profiles/hessian_pmc.json         Hessian per-launch HBM bytes read by bench.py
+  profiles/<tag>_stage_bytes.csv    every kernel of the full pipeline: HBM bytes
+                                    per launch (FETCH x 2, WRITE) and its trace
+                                    time (when the fetchall/writeall passes ran)
 
 HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE are in
 KiB; on gfx950 FETCH_SIZE reads 1/2 of the bytes of a wide coalesced
@@ -83,6 +86,38 @@ def main():
     with open(os.path.join(prof, "hessian_pmc.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
+    stage_bytes(args, prof, kt)
+
+
+def stage_bytes(args, prof, kt):
+    t = args.tag
+    fa = os.path.join(args.src, f"prof_{t}_fetchall", "run_counter_collection.csv")
+    wa = os.path.join(args.src, f"prof_{t}_writeall", "run_counter_collection.csv")
+    if not (os.path.exists(fa) and os.path.exists(wa)):
+        return
+    rows = collections.defaultdict(list)
+    for path in (fa, wa):
+        for r in csv.DictReader(open(path)):
+            if r["Kernel_Name"].startswith("__amd_rocclr"):
+                continue
+            rows[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+    avg_ms = {}
+    for r in csv.DictReader(open(kt)):
+        avg_ms[r["Name"]] = float(r["AverageNs"]) / 1e6
+    kernels = sorted({k for k, _ in rows}, key=lambda k: -avg_ms.get(k, 0.0))
+    with open(os.path.join(prof, f"{t}_stage_bytes.csv"), "w", newline="") as fh:
+        w = csv.writer(fh)
+        w.writerow(["kernel", "trace_avg_ms", "fetch_bytes (2*FETCH_SIZE)", "write_bytes (WRITE_SIZE)",
+                    "hbm_bytes", "GBps_at_trace_avg"])
+        for k in kernels:
+            f = rows.get((k, "FETCH_SIZE"), [0.0])
+            wr = rows.get((k, "WRITE_SIZE"), [0.0])
+            fb = 2 * 1024 * sum(f) / len(f)
+            wb = 1024 * sum(wr) / len(wr)
+            ms = avg_ms.get(k)
+            w.writerow([k[:90], None if ms is None else round(ms, 4), int(fb), int(wb), int(fb + wb),
+                        None if not ms else round((fb + wb) / (ms * 1e-3) / 1e9, 1)])
+    print(f"wrote profiles/{t}_stage_bytes.csv")
 
 
 if __name__ == "__main__":
