@@ -253,6 +253,9 @@ def main():
     ap.add_argument("--gather", choices=("full", "points"), default="full",
                     help="world > 1: all-gather SurfPoints + descriptors, or SurfPoints only "
                          "(descriptors stay on the rank that computed them)")
+    ap.add_argument("--gather-at", choices=("pack", "describe"), default="describe",
+                    help="N > 1: issue batch i's all-gather right after its pack, or after batch i+1's "
+                         "describe starts (beside the latency-bound stage)")
     ap.add_argument("--slab-headroom", type=float, default=1.10,
                     help="fixed per-rank slab capacity = max over ranks of the warm-up slab x this")
     ap.add_argument("--no-exchange-probe", action="store_true",
@@ -388,7 +391,15 @@ def run_rank(args):
     nstep = 0                                          # buffer i & 1 across warmup and timed steps
     timing = [False]
 
-    def gather(i):
+    # --gather-at describe: batch i's all-gather is issued after batch i+1's
+    # describe-start event (surfhip_detector_set_describe_event), so its HBM
+    # writes land beside the latency-bound describe rather than the next
+    # batch's Hessian and NMS; the last batch's goes out after the loop,
+    # inside the timed region
+    ev_desc = None
+    pending = [None]
+
+    def pack(i):
         k = i & 1
         mine = gathered[k].data_ptr() + rank * cap
         if i >= 2:
@@ -396,7 +407,13 @@ def run_rank(args):
         # pack before the next detect_batch reuses the detector's scratch and status
         det.pack_slab_cap(d_pts.data_ptr(), desc_ptr_for_slab, d_cnt.data_ptr(), B, mine, cap)
         ev_packed[k].record(stream)
+
+    def gather(i):
+        k = i & 1
+        mine = gathered[k].data_ptr() + rank * cap
         comm_stream.wait_event(ev_packed[k])
+        if ev_desc is not None:
+            surf.stream_wait_event(comm_stream.cuda_stream, ev_desc)
         ev = None
         if timing[0]:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -413,15 +430,35 @@ def run_rank(args):
             ag_events.append(ev)
         ev_gathered[k].record(comm_stream)
 
+    if exchange and args.gather_at == "describe":
+        ev_desc = surf.event_create()
+        det.set_describe_event(ev_desc)
+
     def step():
         nonlocal nstep
         run_batch()
         if exchange:
-            gather(nstep)
+            if ev_desc is not None:
+                if pending[0] is not None:
+                    gather(pending[0])                # the previous batch, beside this one's describe
+                pack(nstep)
+                pending[0] = nstep
+            else:
+                pack(nstep)
+                gather(nstep)
         nstep += 1
+
+    def flush():
+        if pending[0] is not None:
+            gather(pending[0])
+            pending[0] = None
 
     for i in range(args.warmup):
         step()
+    if ev_desc is not None:
+        # the warm-up's last gather goes out here, outside the timed region
+        # (the first timed step's describe event would otherwise order it)
+        flush()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -431,6 +468,7 @@ def run_rank(args):
     t_start = time.perf_counter()
     for i in range(args.steps):
         step()
+    flush()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -500,7 +538,8 @@ def run_rank(args):
                      "allgather_ms_per_step": None if ag_mean is None else round(ag_mean, 4),
                      "allgather_busbw_GBps": (None if not ag_mean else
                                               round((world - 1) * cap / (ag_mean * 1e-3) / 1e9, 1)),
-                     "overlap": "gather(i) on a comm stream beside compute(i+1)"}
+                     "overlap": ("gather(i) on a comm stream after batch i+1's describe starts"
+                                 if ev_desc is not None else "gather(i) on a comm stream beside compute(i+1)")}
     if world > 1:
         bad = allreduce_max(len(problems))
         if int(bad) and not problems:
@@ -551,7 +590,7 @@ def run_rank(args):
 
     proxy = None
     if world == 1 and args.exchange_proxy > 1 and not args.hessian_only:
-        proxy = exchange_proxy(torch, det, dev, stream, run_batch, d_pts, d_desc, d_cnt, B, args.exchange_proxy,
+        proxy = exchange_proxy(surf, torch, det, dev, stream, run_batch, d_pts, d_desc, d_cnt, B, args.exchange_proxy,
                                args.steps, 1e3 * elapsed / args.steps)
 
     peaks = None
@@ -658,6 +697,9 @@ def run_rank(args):
         else:
             result["cpu_baseline"] = None
         print(json.dumps(result), flush=True)
+    if ev_desc is not None:
+        det.set_describe_event(None)
+        surf.event_destroy(ev_desc)
     det.close()
     if comm is not None:
         comm.close()
@@ -745,19 +787,25 @@ def stream_peaks(surf, torch, dev, stream, nbytes=2 << 30, reps=10):
     return out
 
 
-def exchange_proxy(torch, det, dev, stream, run_batch, d_pts, d_desc, d_cnt, B, nranks, steps, base_ms):
+def exchange_proxy(surf, torch, det, dev, stream, run_batch, d_pts, d_desc, d_cnt, B, nranks, steps, base_ms):
     """Single-GPU proxy of the N-rank exchange's cost to the step: each step
     packs its slab (as the N > 1 loop does) and a comm stream then writes
     (N-1) x slab bytes into a receive buffer by a D2D copy -- the bytes an
-    all-gather lands in this GPU's HBM -- beside the next batch's compute
-    (gather(i) overlaps compute(i+1), as in the real loop).  xGMI link time is
-    not in it (DESIGN.md 5 models that); what it measures is the HBM and CU
+    all-gather lands in this GPU's HBM -- beside the next batch's compute.
+    Two issue points: `pack` (the copy follows the pack at once, so it runs
+    beside the next batch's row sums, Hessian and NMS) and `describe` (the
+    comm stream waits for the next batch's describe-start event,
+    surfhip_detector_set_describe_event: the copy runs beside the
+    latency-bound describe, which leaves HBM idle).  xGMI link time is not in
+    it (DESIGN.md 5 models that); what it measures is the HBM and CU
     contention the received slabs cost the pipeline."""
     out = {"nranks": nranks, "base_ms_per_step": round(base_ms, 4),
-           "note": "D2D copy of (N-1) x slab bytes per step on a comm stream, event-ordered after the pack; "
-                   "the xGMI transfer itself is modelled in DESIGN.md 5"}
+           "note": "D2D copy of (N-1) x slab bytes per step on a comm stream, event-ordered after the pack "
+                   "(at: pack) or after the next batch's describe start (at: describe); the xGMI transfer "
+                   "itself is modelled in DESIGN.md 5"}
     total = det.batch_total(B)
     cs = torch.cuda.Stream(dev)
+    ev_desc = surf.event_create()
     for mode in ("full", "points"):
         used = det.slab_bytes(B, total, desc=mode == "full")
         cap = (int(used * 1.10) + 64 + 255) // 256 * 256
@@ -765,42 +813,59 @@ def exchange_proxy(torch, det, dev, stream, run_batch, d_pts, d_desc, d_cnt, B, 
         src = torch.empty((nranks - 1) * cap, dtype=torch.uint8, device=dev)
         dst = [torch.empty((nranks - 1) * cap, dtype=torch.uint8, device=dev) for _ in range(2)]
         src.fill_(1)
-        packed = [torch.cuda.Event() for _ in range(2)]
-        landed = [torch.cuda.Event() for _ in range(2)]
-        cev = []
+        res = {"slab_bytes": used, "received_bytes_per_step": (nranks - 1) * cap}
+        for at in ("pack", "describe"):
+            packed = [torch.cuda.Event() for _ in range(2)]
+            landed = [torch.cuda.Event() for _ in range(2)]
+            cev = []
+            pending = [None]
+            det.set_describe_event(ev_desc if at == "describe" else None)
 
-        def one(i, timed):
-            k = i & 1
-            run_batch()
-            if i >= 2:
-                stream.wait_event(landed[k])
-            det.pack_slab_cap(d_pts.data_ptr(), d_desc.data_ptr() if mode == "full" else None, d_cnt.data_ptr(),
-                              B, slab[k].data_ptr(), cap)
-            packed[k].record(stream)
-            cs.wait_event(packed[k])
-            with torch.cuda.stream(cs):
-                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if timed else None
-                if ev:
-                    ev[0].record(cs)
-                dst[k].copy_(src, non_blocking=True)
-                if ev:
-                    ev[1].record(cs)
-                    cev.append(ev)
-            landed[k].record(cs)
+            def copy(k, timed):
+                cs.wait_event(packed[k])
+                if at == "describe":
+                    surf.stream_wait_event(cs.cuda_stream, ev_desc)
+                with torch.cuda.stream(cs):
+                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if timed else None
+                    if ev:
+                        ev[0].record(cs)
+                    dst[k].copy_(src, non_blocking=True)
+                    if ev:
+                        ev[1].record(cs)
+                        cev.append(ev)
+                landed[k].record(cs)
 
-        for i in range(3):
-            one(i, False)
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for i in range(steps):
-            one(3 + i, True)
-        torch.cuda.synchronize(dev)
-        ms = 1e3 * (time.perf_counter() - t0) / steps
-        cms = float(np.mean([a.elapsed_time(b) for a, b in cev]))
-        out[mode] = {"slab_bytes": used, "received_bytes_per_step": (nranks - 1) * cap,
-                     "ms_per_step": round(ms, 4), "copy_ms": round(cms, 4),
-                     "slowdown": round(ms / base_ms, 4)}
+            def one(i, timed):
+                k = i & 1
+                run_batch()
+                if at == "describe" and pending[0] is not None:
+                    copy(pending[0], timed)          # batch i-1's slab, beside batch i's describe
+                if i >= 2:
+                    stream.wait_event(landed[k])
+                det.pack_slab_cap(d_pts.data_ptr(), d_desc.data_ptr() if mode == "full" else None,
+                                  d_cnt.data_ptr(), B, slab[k].data_ptr(), cap)
+                packed[k].record(stream)
+                if at == "pack":
+                    copy(k, timed)
+                else:
+                    pending[0] = k
+
+            for i in range(3):
+                one(i, False)
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for i in range(steps):
+                one(3 + i, True)
+            if at == "describe":                 # the last batch's slab, inside the timed region
+                copy(pending[0], True)
+            torch.cuda.synchronize(dev)
+            ms = 1e3 * (time.perf_counter() - t0) / steps
+            cms = float(np.mean([a.elapsed_time(b) for a, b in cev]))
+            res[at] = {"ms_per_step": round(ms, 4), "copy_ms": round(cms, 4), "slowdown": round(ms / base_ms, 4)}
+        det.set_describe_event(None)
+        out[mode] = res
         del slab, src, dst
+    surf.event_destroy(ev_desc)
     return out
 
 

@@ -135,6 +135,8 @@ _sigs = {
     "surfhip_dump_append": (_i, [C.c_char_p, _vp, _sz, _i, _i, C.POINTER(SurfParam), C.c_longlong]),
     "surfhip_build_info": (C.c_char_p, []),
     "surfhip_stream_run": (_i, [_i, _vp, _vp, _sz, _vp]),
+    "surfhip_stream_wait_event": (_i, [_vp, _vp]),
+    "surfhip_detector_set_describe_event": (_i, [_vp, _vp]),
     "surfhip_stream_bytes": (_sz, [_i, _sz]),
 }
 for _name, (_res, _args) in _sigs.items():
@@ -242,6 +244,21 @@ def download_ptr(ptr: int, dtype, count: int) -> np.ndarray:
     return out
 
 
+def event_create() -> int:
+    e = C.c_void_p()
+    check(_lib.surfhip_event_create(C.byref(e)), "event_create")
+    return e.value
+
+
+def event_destroy(event: int) -> None:
+    check(_lib.surfhip_event_destroy(event), "event_destroy")
+
+
+def stream_wait_event(stream, event: int) -> None:
+    """Make `stream` (a hipStream_t handle) wait for the event's last record."""
+    check(_lib.surfhip_stream_wait_event(stream, event), "stream_wait_event")
+
+
 STREAM_MODES = {"copy": 0, "read": 1, "write": 2}
 
 
@@ -324,6 +341,11 @@ class Detector:
         check(_lib.surfhip_detect_batch_next(self.h, frames_ptr, nframes, pitch, stride, points_ptr, desc_ptr,
                                              counts_ptr, next_ptr, next_nframes, next_pitch, next_stride),
               "detect_batch_next")
+
+    def set_describe_event(self, event: int | None) -> None:
+        """Record `event` (event_create) before each describe stage
+        (surfhip_detector_set_describe_event); None stops it."""
+        check(_lib.surfhip_detector_set_describe_event(self.h, event), "set_describe_event")
 
     def drain(self) -> None:
         """Order the side stream's pending prefetch before the detector

@@ -102,6 +102,7 @@ struct surfhip_detector {
     // [1] on it after the u8 kernels, [2] on the side stream after the
     // integral-image kernels (only when the plan has some: hev_side)
     hipEvent_t hev[SURFHIP_MAX_HESS_EV][3]{};
+    hipEvent_t desc_ev = nullptr;       // caller's event, recorded before each describe stage
     bool hev_side[SURFHIP_MAX_HESS_EV]{};
     int hev_n = 0;
     int last_nframes = 0;
@@ -254,6 +255,11 @@ int surfhip_event_destroy(void* ev)
 int surfhip_event_record(void* ev, void* stream)
 {
     HIPCHK(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream));
+    return SURFHIP_OK;
+}
+int surfhip_stream_wait_event(void* stream, void* ev)
+{
+    HIPCHK(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)ev, 0));
     return SURFHIP_OK;
 }
 int surfhip_event_synchronize(void* ev)
@@ -805,6 +811,7 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
                        d->cap, nframes, points, d->max_pts, counts, d->offsets, d->order, d->status, s));
     if (prof) HIPCHK(hipEventRecord(d->ev[4], s));
     if (pipe && !pref_nms) HIPCHK(prefetch_next());
+    if (d->desc_ev) HIPCHK(hipEventRecord(d->desc_ev, s));
     if (desc)
         HIPCHK(launch_describe(d->ii, d->P, points, d->max_pts, counts, d->offsets, d->order, d->work, nframes, desc,
                                d->status + 64, s, pipe && !pref_nms && !iiw, d->cus));
@@ -813,6 +820,13 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
     d->last_frames = frames;
     d->last_pitch = pitch;
     d->last_fstride = (long long)stride;
+    return SURFHIP_OK;
+}
+
+int surfhip_detector_set_describe_event(surfhip_detector* d, void* ev)
+{
+    if (!d) return SURFHIP_ERR_INVALID;
+    d->desc_ev = (hipEvent_t)ev;
     return SURFHIP_OK;
 }
 

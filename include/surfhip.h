@@ -95,6 +95,7 @@ int  surfhip_event_create(void** ev);             /* cudaEventCreate (GpuTimer) 
 int  surfhip_event_destroy(void* ev);
 int  surfhip_event_record(void* ev, void* stream);
 int  surfhip_event_synchronize(void* ev);
+int  surfhip_stream_wait_event(void* stream, void* ev);  /* cudaStreamWaitEvent */
 int  surfhip_event_elapsed(float* ms, void* start, void* stop);
 
 /* ----------------------------------------------------------- detector --
@@ -157,6 +158,14 @@ int surfhip_detect_batch_next(surfhip_detector* det, const uint8_t* d_frames, in
  * detector's stream: after drain, synchronising that stream means
  * next_frames are no longer read.  The prefetch stays valid. */
 int surfhip_detector_drain(surfhip_detector* det);
+
+/* Record `event` (a surfhip_event_create / hipEvent_t) on the detector's
+ * stream right before the describe stage of every following detect_batch /
+ * detect_batch_next call (NULL: no longer).  A multi-GPU caller makes its
+ * comm stream wait on it so the previous batch's all-gather lands beside the
+ * latency-bound describe instead of the HBM-bound Hessian and NMS (SURVEY
+ * 8e; no reference counterpart). */
+int surfhip_detector_set_describe_event(surfhip_detector* det, void* event);
 
 /* Surfor::detectAndCompute (surf.cpp:205-355) for one frame, synchronous.
  * Writes min(found, max_pts) SurfPoints to d_points, returns the count in
