@@ -51,6 +51,14 @@ _Zk_branch:
 \tbuffer_store_dwordx4 v[2:5], v10, s[16:19], 0 offen
 \ts_branch .LBB0_1
 \tv_mov_b32_e32 v2, 0
+.LBB0_1:
+\tv_mov_b32_e32 v3, 0
+_Zk_branch_far:
+\tbuffer_store_dwordx4 v[2:5], v10, s[16:19], 0 offen
+\ts_branch .LBB0_2
+.LBB0_2:
+\ts_nop 0
+\tv_mov_b32_e32 v3, 0
 """
 
 
@@ -60,7 +68,9 @@ def test_scanner_rule(tmp_path):
     p.write_text(LISTING)
     counts, hits = sc.scan(str(p), None)
     flagged = {k for k, v in counts.items() if v[1]}
-    assert flagged == {"_Zk_sgpr_next", "_Zk_const_one", "_Zk_global_one"}, flagged
+    # (_Zk_branch: the overwrite one wait state away through the s_branch;
+    # _Zk_branch_far: two)
+    assert flagged == {"_Zk_sgpr_next", "_Zk_const_one", "_Zk_global_one", "_Zk_branch"}, flagged
     assert sc.need("s70") == 1 and sc.need("vcc_lo") == 1 and sc.need("0") == 2 and sc.need("-") == 2
 
 

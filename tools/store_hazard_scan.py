@@ -11,9 +11,9 @@ hazard recognizer gives 0 and 1.  8-B stores need none.
 Default: the device code objects inside cuda-surf_amd/libsurfhip.so
 (llvm-objdump --offloading, then -d).  .s files (hipcc --cuda-device-only
 -S) are read as they are.  Wait states: one per instruction between the store
-and the overwrite, s_nop k counting k + 1.  Branches end the search (a
-conservative miss is possible across blocks).  Exit status 1 if any store
-violates the measured rule.
+and the overwrite, s_nop k counting k + 1; branches are followed (both ways
+for a conditional one).  Exit status 1 if any store violates the measured
+rule.
 """
 from __future__ import annotations
 
@@ -61,11 +61,88 @@ def need(soff: str) -> int:
     return 1 if re.match(r"^(s\d+|vcc_\w+|m0|ttmp\d+)$", soff) else 2
 
 
+ADDR = re.compile(r"//\s*([0-9A-Fa-f]+):")
+TARGET = re.compile(r"<(\S+)\+0x([0-9a-f]+)>")
+HEADER = re.compile(r"^([0-9a-f]+) <(\S+)>:")
+
+
+def _index(lines):
+    """label / address -> line index, for following branches"""
+    labels, addr, base = {}, {}, {}
+    for i, line in enumerate(lines):
+        m = HEADER.match(line)
+        if m:
+            base[m.group(2)] = int(m.group(1), 16)
+            continue
+        if line.startswith(".L") and line.rstrip().endswith(":") or re.match(r"^\.LBB\S+:", line):
+            labels[line.split(":")[0].strip()] = i
+        a = ADDR.search(line)
+        if a:
+            addr[int(a.group(1), 16)] = i
+    return labels, addr, base
+
+
+def _targets(s, labels, addr, base):
+    """line indices a branch instruction may continue at (besides falling
+    through for a conditional one)"""
+    t = TARGET.search(s)
+    if t and t.group(1) in base:
+        i = addr.get(base[t.group(1)] + int(t.group(2), 16))
+        return [i] if i is not None else []
+    parts = s.split()
+    if len(parts) > 1 and parts[1] in labels:
+        return [labels[parts[1]]]
+    return []
+
+
 def scan(path: str, within: int | None):
     lines = open(path).read().split("\n")
+    labels, addr, base = _index(lines)
     cur = None
     hits = {}
     counts = {}
+
+    def walk(j, ws, lim, lo, hi, depth):
+        """first VALU write of v[lo:hi] at <= lim wait states from line j
+        on (branches followed, conditional ones both ways), or None"""
+        while j < len(lines) and depth < 8:
+            t = lines[j].split("//")[0]
+            s = t.strip()
+            j += 1
+            if not s or s.startswith(";") or s.startswith(".") and not s.endswith(":"):
+                continue
+            if re.match(r"^\S+:", t) or HEADER.match(lines[j - 1]):
+                continue
+            if s.startswith(("s_setpc", "s_endpgm", "s_trap")):
+                return None
+            if s.startswith("s_branch") or s.startswith("s_cbranch"):
+                ws += 1
+                if ws > lim:
+                    return None
+                for tj in _targets(lines[j - 1], labels, addr, base):
+                    h = walk(tj, ws, lim, lo, hi, depth + 1)
+                    if h:
+                        return h
+                if s.startswith("s_branch"):
+                    return None
+                continue
+            n = NOP.match(t)
+            if n:
+                ws += int(n.group(1)) + 1
+                if ws > lim:
+                    return None
+                continue
+            v = VALU.match(t)
+            if v and not v.group(1).startswith(("v_cmp", "v_readlane", "v_readfirstlane", "v_cmpx")):
+                a = int(v.group(2) or v.group(4))
+                z = int(v.group(3) or v.group(4))
+                if not (z < lo or a > hi):
+                    return (j, ws, s.split()[0])
+            ws += 1
+            if ws > lim:
+                return None
+        return None
+
     for i, line in enumerate(lines):
         m = FUNC.match(line)
         if m and not line.startswith("."):
@@ -80,32 +157,10 @@ def scan(path: str, within: int | None):
         c = counts.setdefault(cur, [0, 0])
         c[0] += 1
         lim = need(soff) - 1 if within is None else within
-        ws = 0
-        for j in range(i + 1, min(len(lines), i + 40)):
-            t = lines[j].split("//")[0]
-            s = t.strip()
-            if not s or s.startswith(";") or s.startswith("."):
-                continue
-            if re.match(r"^\S+:", t) or s.startswith("s_branch") or s.startswith("s_cbranch") or \
-                    s.startswith("s_setpc") or s.startswith("s_endpgm"):
-                break
-            n = NOP.match(t)
-            if n:
-                ws += int(n.group(1)) + 1
-                if ws > lim:
-                    break
-                continue
-            v = VALU.match(t)
-            if v and not v.group(1).startswith(("v_cmp", "v_readlane", "v_readfirstlane", "v_cmpx")):
-                a = int(v.group(2) or v.group(4))
-                z = int(v.group(3) or v.group(4))
-                if not (z < lo or a > hi):
-                    c[1] += 1
-                    hits.setdefault(cur, []).append((j + 1, ws, soff, s.split()[0]))
-                    break
-            ws += 1
-            if ws > lim:
-                break
+        h = walk(i + 1, 0, lim, lo, hi, 0)
+        if h:
+            c[1] += 1
+            hits.setdefault(cur, []).append((h[0], h[1], soff, h[2]))
     return counts, hits
 
 
