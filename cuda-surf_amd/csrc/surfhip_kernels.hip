@@ -914,10 +914,10 @@ hipError_t launch_hessian(const uint8_t* frames, int pitch, long long fstride, c
             // (iiw 2, only with the default 93: this launch writes the integral)
             const bool wr0 = plan.iiw == 2 && ii_out && rowseg;
 #define P0_CASE(BB, GG)                                                                                          \
-    else if (pb == BB && pg == GG) k_hess_p0<BB, GG, 1, false><<<gp, 64 * (1 + GG), 0, s>>>(                       \
+    else if (pb == BB && pg == GG) k_hess_p0<BB, GG, SURF_P0_PLANE_NT, false><<<gp, 64 * (1 + GG), 0, s>>>(        \
         frames, pitch, fstride, resp, P, h_oct[0], plan.q0_strips, nframes, nullptr, nullptr, 0);
             if (wr0 && pb == 9 && pg == 3)
-                k_hess_p0<9, 3, 1, true><<<gp, 64 * 4, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
+                k_hess_p0<9, 3, SURF_P0_PLANE_NT, true><<<gp, 64 * 4, 0, s>>>(frames, pitch, fstride, resp, P, h_oct[0],
                                                                plan.q0_strips, nframes, rowseg, ii_out, plan.rs_rows);
             P0_CASE(9, 5) P0_CASE(9, 4) P0_CASE(9, 3) P0_CASE(9, 2) P0_CASE(9, 1) P0_CASE(3, 2) P0_CASE(3, 3)
 #undef P0_CASE

@@ -22,7 +22,7 @@ for r in $(seq 1 $PAIRS); do
     esac
     n=$(echo "$v" | tr -c 'A-Za-z0-9_\n' '_')
     env SURFHIP_LIB_DIR=$LD "${EV[@]}" timeout -k 10 180 python3 bench.py --steps 30 --warmup 3 --no-cpu \
-        --no-exchange-probe "$@" > $O/ab_${TAG}_${n}_$r.json 2> $O/ab_${TAG}_${n}_$r.err \
+        --no-exchange-probe --no-stream-peak "$@" > $O/ab_${TAG}_${n}_$r.json 2> $O/ab_${TAG}_${n}_$r.err \
         || { tail -5 $O/ab_${TAG}_${n}_$r.err; exit 1; }
     python3 - $O/ab_${TAG}_${n}_$r.json "$v" <<'PY'
 import json, sys
