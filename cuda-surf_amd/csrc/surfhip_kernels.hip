@@ -2454,20 +2454,6 @@ struct RotScratch {
 #ifndef SURF_ROT_WPE
 #define SURF_ROT_WPE 3              // 3 waves per SIMD: <= 168 VGPRs (the 128-D form took 185: 2 waves)
 #endif
-// Haar table (round 6): the rotated window's samples lie
-// on the keypoint's axis-aligned grid (iy + i step, ix + j step,
-// surfd.cu:2404-2417), so their two Haar responses do not depend on the
-// rotation.  A wave computes them for a band of kRotBR grid rows at once --
-// lane = grid column, the 12 integral corners of every row of the band
-// issued together (coalesced along the row, many in flight) -- into an LDS
-// table, and the cell owners' walk reads one 8-byte entry per sample instead
-// of its 12 dependent gathers (the walk's order, membership tests and float
-// operations are unchanged: descriptors bit-identical to the gather form,
-// SURF_ROT_TABLE=0).
-#ifndef SURF_ROT_TABLE
-#define SURF_ROT_TABLE 1
-#endif
-constexpr int kRotBR = 8;           // grid rows per table band
 template <int NB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SURF_ROT_WPE))) void k_describe_rot(const int32_t* __restrict__ ii, FrameParams P,
                                                       surfhip_point* __restrict__ pts, int max_pts,
@@ -2476,9 +2462,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SURF_ROT_WP
 {
     constexpr int WSZ = 4, NC = WSZ + 1, NF = WSZ * WSZ * NB;
     __shared__ RotScratch sr[4];
-#if SURF_ROT_TABLE
-    __shared__ int2 s_haar[4][kRotBR][64];   // (wavelet1, wavelet2) of a band's grid rows, lane = grid column
-#endif
     const unsigned lane = lane_id();
     const int w = threadIdx.x >> 6;
     const int total = offsets[nframes];
@@ -2605,51 +2588,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SURF_ROT_WP
             for (int b = 0; b < NB; b++) accp[h][b] = v2f32{0.f, 0.f};
         int si = i0, sj = 0;
         if (si <= i1) { row_range(si); sj = rlo; }
-#if SURF_ROT_TABLE
-        // the band's table column of this lane: grid column tj, image column tc
-        const int tj = (int)lane - iradius;
-        const int tc = ix + tj * step;
-        const __amdgpu_buffer_rsrc_t IR =
-            __builtin_amdgcn_make_buffer_rsrc((void*)I, (short)0, (int)(P.ii_stride * 4), 0x00020000);
-        // corners of wavelet1 / wavelet2 at (tc, r, hs) (box, surfd.cu:334-343):
-        // integral rows r - hs, r, r + 1, r + hs + 1 at columns tc - hs, tc,
-        // tc + 1, tc + hs + 1 (12 distinct points); outside the frame's buffer
-        // a load reads 0 (those samples fail the walk's bounds test)
-        const int cm = (tc - hs) * 4, c0b = tc * 4, c1b = (tc + 1) * 4, cp = (tc + hs + 1) * 4;
-        const int ipb = ip * 4;
-        auto bl = [&](int off) -> uint32_t { return __builtin_amdgcn_raw_buffer_load_b32(IR, off, 0, 0); };
-        for (int b0 = -iradius; b0 <= iradius; b0 += kRotBR) {
-            const int b1 = min(b0 + kRotBR - 1, iradius);
-            wave_sync();                      // the previous band's entries are read
-            // rows of a band in groups of KG, a group's 12 KG loads in flight
-            // (128-D: 2 rows, inside the 168-VGPR budget; 64-D: 4)
-            constexpr int KG = NB == 8 ? 2 : 4;
-#pragma unroll
-            for (int k0 = 0; k0 < kRotBR; k0 += KG) {
-                uint32_t q[KG][12];
-#pragma unroll
-                for (int k = 0; k < KG; k++) {
-                    const int r = iy + (b0 + k0 + k) * step;
-                    const int A = (r - hs) * ipb, B = r * ipb, C = (r + 1) * ipb, D = (r + hs + 1) * ipb;
-                    q[k][0] = bl(A + cm); q[k][1] = bl(A + c0b); q[k][2] = bl(A + c1b); q[k][3] = bl(A + cp);
-                    q[k][4] = bl(B + cm); q[k][5] = bl(B + cp);
-                    q[k][6] = bl(C + cm); q[k][7] = bl(C + cp);
-                    q[k][8] = bl(D + cm); q[k][9] = bl(D + c0b); q[k][10] = bl(D + c1b); q[k][11] = bl(D + cp);
-                }
-#pragma unroll
-                for (int k = 0; k < KG; k++) {
-                    const uint32_t* v = q[k];
-                    // b1 - b2 = wavelet1, b3 - b4 = wavelet2 (uint32, the reference's int sums)
-                    const uint32_t w1 = (v[7] + v[0] - v[3] - v[6]) - (v[11] + v[4] - v[5] - v[8]);
-                    const uint32_t w2 = (v[11] + v[1] - v[3] - v[9]) - (v[10] + v[0] - v[2] - v[8]);
-                    s_haar[w][k0 + k][lane] = make_int2((int32_t)w1, (int32_t)w2);
-                }
-            }
-            wave_sync();
-        while (si <= i1 && si <= b1) {
-#else
         while (si <= i1) {
-#endif
             if (sj > rhi) {
                 si += 2;
                 if (si <= i1) { row_range(si); sj = rlo; }
@@ -2674,10 +2613,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SURF_ROT_WP
 #ifdef SURF_DIAG_ROT_NOLOAD
             const float dxx = (weight * (float)(r * 7 - c)) * INV255;
             const float dyy = (weight * (float)(c * 3 + r)) * INV255;
-#elif SURF_ROT_TABLE
-            const int2 hv = s_haar[w][si - b0][cj + iradius];
-            const float dxx = (weight * (float)hv.y) * INV255;
-            const float dyy = (weight * (float)hv.x) * INV255;
 #else
             const float dxx = (weight * (float)wavelet2(I, ip, c, r, hs)) * INV255;
             const float dyy = (weight * (float)wavelet1(I, ip, c, r, hs)) * INV255;
@@ -2725,9 +2660,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SURF_ROT_WP
                 put(I6{}, I7{}, fabsf(dy), dx < 0);
             }
         }
-#if SURF_ROT_TABLE
-        }                                     // band
-#endif
         wave_sync();                          // orientation scratch is dead: reuse it
 #pragma unroll
         for (int q = 0; q < 4; q++)
