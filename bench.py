@@ -253,7 +253,7 @@ def main():
     ap.add_argument("--gather", choices=("full", "points"), default="full",
                     help="world > 1: all-gather SurfPoints + descriptors, or SurfPoints only "
                          "(descriptors stay on the rank that computed them)")
-    ap.add_argument("--gather-at", choices=("pack", "describe"), default="describe",
+    ap.add_argument("--gather-at", choices=("pack", "describe"), default="pack",
                     help="N > 1: issue batch i's all-gather right after its pack, or after batch i+1's "
                          "describe starts (beside the latency-bound stage)")
     ap.add_argument("--slab-headroom", type=float, default=1.10,
