@@ -2022,37 +2022,6 @@ __device__ __forceinline__ int32_t wavelet2(const uint32_t* __restrict__ I, int 
     return (int32_t)(box(I, ip, x + size, y + size, x, y - size) - box(I, ip, x, y + size, x - size, y - size));
 }
 
-// Both Haar responses at (x, y) of half-size s -- wavelet1 and wavelet2,
-// the four getSum boxes of surfd.cu:1171-1182 -- from their 12 distinct
-// integral corners (rows y - s, y, y + 1, y + s + 1; columns x - s, x,
-// x + 1, x + s + 1) in 10 buffer loads: the adjacent (x, x + 1) pairs of rows
-// y - s and y + s + 1 are one 8-byte load each.  The gathers of the rotated
-// descriptor's walk and the orientation are address-bound (DESIGN §6 item
-// 22): two fewer addresses per sample, and 32-bit offsets instead of 64-bit
-// pointers.  uint32 sums as getSum's int adds (wrapping), so the values are
-// wavelet1 / wavelet2's exactly.
-#ifndef SURF_HAAR_PAIR
-#define SURF_HAAR_PAIR 1            // haar_pair's 10 loads (0: wavelet1 + wavelet2, 12 gathers; A/B)
-#endif
-struct HaarPair {
-    int32_t w1, w2;
-};
-__device__ __forceinline__ HaarPair haar_pair(__amdgpu_buffer_rsrc_t R, int ipb, int x, int y, int s)
-{
-    const int A = (y - s) * ipb, B = y * ipb, C = (y + 1) * ipb, D = (y + s + 1) * ipb;
-    const int xm = (x - s) * 4, x0 = x * 4, xp = (x + s + 1) * 4;
-    auto ld = [&](int o) -> uint32_t { return __builtin_amdgcn_raw_buffer_load_b32(R, o, 0, 0); };
-    const uint32_t a_m = ld(A + xm), a_p = ld(A + xp);
-    const v2u32 a_01 = __builtin_amdgcn_raw_buffer_load_b64(R, A + x0, 0, 0);
-    const uint32_t b_m = ld(B + xm), b_p = ld(B + xp), c_m = ld(C + xm), c_p = ld(C + xp);
-    const uint32_t d_m = ld(D + xm), d_p = ld(D + xp);
-    const v2u32 d_01 = __builtin_amdgcn_raw_buffer_load_b64(R, D + x0, 0, 0);
-    HaarPair h;
-    h.w1 = (int32_t)((c_p + a_m - a_p - c_m) - (d_p + b_m - b_p - d_m));
-    h.w2 = (int32_t)((d_p + a_01.x - a_p - d_01.x) - (d_01.y + a_m - a_01.y - d_m));
-    return h;
-}
-
 // dFastAtan2 (surfd.cu:114-126)
 __device__ __forceinline__ float fast_atan2(float y, float x)
 {
@@ -2170,11 +2139,6 @@ __device__ float orientation_wave(const uint32_t* __restrict__ I, const FramePar
     const int pixsi = f2i_rz(2.f * scale + 1.6f);
     const int pixsi2 = f2i_rz(scale + 0.8f);
     const int ixo = f2i_rn(at.x), iyo = f2i_rn(at.y);
-#if SURF_HAAR_PAIR
-    const __amdgpu_buffer_rsrc_t IR =
-        __builtin_amdgcn_make_buffer_rsrc((void*)I, (short)0, (int)(P.ii_stride * 4), 0x00020000);
-    const int ipb = ip * 4;
-#endif
     for (int t = lane; t < 6 * 72; t += 64) (&S.bmask[0][0])[t] = 0ull;
     wave_sync();
     for (int t = lane; t < 361; t += 64) {
@@ -2185,14 +2149,8 @@ __device__ float orientation_wave(const uint32_t* __restrict__ I, const FramePar
         if (yy + pixsi + 2 < P.iH && yy - pixsi > -1 && xx + pixsi + 2 < P.W + 1 && xx - pixsi > -1) {
             const int distsq = y1 * y1 + x1 * x1;
             if ((float)distsq < 81.5f) {
-#if SURF_HAAR_PAIR
-                const HaarPair hp = haar_pair(IR, ipb, xx, yy, pixsi);
-                const float dx = (float)hp.w2 * INV255;
-                const float dy = (float)hp.w1 * INV255;
-#else
                 const float dx = (float)wavelet2(I, ip, xx, yy, pixsi) * INV255;
                 const float dy = (float)wavelet1(I, ip, xx, yy, pixsi) * INV255;
-#endif
                 const float mag = sqrtf(dx * dx + dy * dy);
                 if (mag > 0.f) {
                     angle = fast_atan2(dy, dx);
@@ -2630,11 +2588,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SURF_ROT_WP
             for (int b = 0; b < NB; b++) accp[h][b] = v2f32{0.f, 0.f};
         int si = i0, sj = 0;
         if (si <= i1) { row_range(si); sj = rlo; }
-#if SURF_HAAR_PAIR
-        const __amdgpu_buffer_rsrc_t IR =
-            __builtin_amdgcn_make_buffer_rsrc((void*)I, (short)0, (int)(P.ii_stride * 4), 0x00020000);
-        const int ipb = ip * 4;
-#endif
         while (si <= i1) {
             if (sj > rhi) {
                 si += 2;
@@ -2660,10 +2613,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SURF_ROT_WP
 #ifdef SURF_DIAG_ROT_NOLOAD
             const float dxx = (weight * (float)(r * 7 - c)) * INV255;
             const float dyy = (weight * (float)(c * 3 + r)) * INV255;
-#elif SURF_HAAR_PAIR
-            const HaarPair hp = haar_pair(IR, ipb, c, r, hs);
-            const float dxx = (weight * (float)hp.w2) * INV255;
-            const float dyy = (weight * (float)hp.w1) * INV255;
 #else
             const float dxx = (weight * (float)wavelet2(I, ip, c, r, hs)) * INV255;
             const float dyy = (weight * (float)wavelet1(I, ip, c, r, hs)) * INV255;
