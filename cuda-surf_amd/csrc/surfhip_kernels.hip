@@ -1830,7 +1830,11 @@ __global__ __launch_bounds__(1024) void k_sort(const surfhip_point* __restrict__
     // times (octave, layer, y); the band order sweeps it once, so the few
     // hundred keypoints an XCD describes at a time share their integral-image
     // rows in that XCD's L2.
-    // A counting sort by band: the order within a band is free (describe
+    // (SURF_DESC_BAND_SHIFT: log2 of the band height, A/B)
+#ifndef SURF_DESC_BAND_SHIFT
+#define SURF_DESC_BAND_SHIFT 4
+#endif
+// A counting sort by band: the order within a band is free (describe
     // writes each descriptor at its canonical index; the order only groups
     // the keypoints an XCD describes at a time), so two passes of LDS atomics
     // replace round 2's second bitonic sort (78 barrier passes for 4,096 keys).
@@ -1844,7 +1848,7 @@ __global__ __launch_bounds__(1024) void k_sort(const surfhip_point* __restrict__
     __syncthreads();
     auto band_of = [&](int t) -> uint32_t {
         const float y = out[(size_t)f * max_pts + t].y;
-        return min((uint32_t)max(y, 0.f) >> 4, (uint32_t)NBAND - 1u);
+        return min((uint32_t)max(y, 0.f) >> SURF_DESC_BAND_SHIFT, (uint32_t)NBAND - 1u);
     };
     for (int t = threadIdx.x; t < keep; t += blockDim.x) atomicAdd(&bc[band_of(t)], 1u);
     __syncthreads();
