@@ -2134,8 +2134,9 @@ struct OriScratch {
 };
 
 // assignOrientationApprox (surfd.cu:1711-1960) for one keypoint on one wave.
+// lut1: the orientation weights (lookup1, c_tab.lut1 or an LDS copy of it)
 __device__ float orientation_wave(const uint32_t* __restrict__ I, const FrameParams& P, const surfhip_point& p,
-                                  OriScratch& S, unsigned lane)
+                                  OriScratch& S, unsigned lane, const float* lut1 = c_tab.lut1)
 {
     const int ip = P.ip;
     const DescAt at = ori_at(P.doubled, p);
@@ -2159,7 +2160,7 @@ __device__ float orientation_wave(const uint32_t* __restrict__ I, const FramePar
                 if (mag > 0.f) {
                     angle = fast_atan2(dy, dx);
                     hid = f2i_rz((float)(((double)angle + M_PI_D) / (double)SEP_ANGLE_F)) % 72;
-                    psum = c_tab.lut1[distsq] * mag;
+                    psum = lut1[distsq] * mag;
                 }
             }
         }
@@ -2455,6 +2456,9 @@ struct RotScratch {
     };
 };
 
+#ifndef SURF_ROT_LDS_LUT
+#define SURF_ROT_LDS_LUT 1
+#endif
 #ifndef SURF_ROT_WPE
 #define SURF_ROT_WPE 3              // 3 waves per SIMD: <= 168 VGPRs (the 128-D form took 185: 2 waves)
 #endif
@@ -2466,6 +2470,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SURF_ROT_WP
 {
     constexpr int WSZ = 4, NC = WSZ + 1, NF = WSZ * WSZ * NB;
     __shared__ RotScratch sr[4];
+#if SURF_ROT_LDS_LUT
+    // the Gaussian weight tables in LDS: each sample's weight is one
+    // lane-indexed read, from LDS instead of a global load on the walk's
+    // dependency chain (same values)
+    __shared__ float s_lut1[83], s_lut2[40];
+    for (int t = threadIdx.x; t < 83; t += blockDim.x) s_lut1[t] = c_tab.lut1[t];
+    for (int t = threadIdx.x; t < 40; t += blockDim.x) s_lut2[t] = c_tab.lut2[t];
+    __syncthreads();
+    const float* const lut1 = s_lut1;
+    const float* const lut2 = s_lut2;
+#else
+    const float* const lut1 = c_tab.lut1;
+    const float* const lut2 = c_tab.lut2;
+#endif
     const unsigned lane = lane_id();
     const int w = threadIdx.x >> 6;
     const int total = offsets[nframes];
@@ -2491,7 +2509,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SURF_ROT_WP
 #ifdef SURF_DIAG_NOORI
         const float ori = 0.3f;
 #else
-        const float ori = orientation_wave(I, P, p, S.ori, lane);
+        const float ori = orientation_wave(I, P, p, S.ori, lane, lut1);
 #endif
         if (lane == 0) pp->ori = ori;
 #ifdef SURF_DIAG_NODESC
@@ -2613,7 +2631,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SURF_ROT_WP
             if (ri != cri || ci != cci) continue;
             const int r = iy + si * step, c = ix + cj * step;
             if (!(r >= 1 + hs && r < rlim && c >= 1 + hs && c < clim)) continue;
-            const float weight = c_tab.lut2[f2i_rz(rpos * rpos + cpos * cpos)];
+            const float weight = lut2[f2i_rz(rpos * rpos + cpos * cpos)];
 #ifdef SURF_DIAG_ROT_NOLOAD
             const float dxx = (weight * (float)(r * 7 - c)) * INV255;
             const float dyy = (weight * (float)(c * 3 + r)) * INV255;
