@@ -1173,6 +1173,9 @@ __device__ __forceinline__ OctView make_view(const float* F, const OctaveParams&
     return V;
 }
 
+#ifndef SURF_NMS_GLOBAL_ROW3
+#define SURF_NMS_GLOBAL_ROW3 0        // (A/B) the neighbour rows of three by global instead of buffer loads
+#endif
 // Wave-aggregated append: one atomic per wave for all its `ok` lanes.
 __device__ __forceinline__ int wave_append(bool ok, int* counter)
 {
@@ -1357,10 +1360,18 @@ __device__ __forceinline__ void nms_scan_item(const float* __restrict__ resp, co
                     if (HK && pl < 2) {
                         a0 = V(pl, rr, c - 1); a1 = V(pl, rr, c); a2 = V(pl, rr, c + 1);
                     } else {
+#if SURF_NMS_GLOBAL_ROW3
+                        // (a global 12-byte load: inside the plane -- the block
+                        // border keeps r +- 1, c +- 1 in the sample grid)
+                        typedef float v3f32a4 __attribute__((ext_vector_type(3), aligned(4)));
+                        const v3f32a4 t3 = *reinterpret_cast<const v3f32a4*>(V.F + V.cur + pl * V.osize + rr * V.sp + c - 1);
+                        a0 = t3.x; a1 = t3.y; a2 = t3.z;
+#else
                         typedef uint32_t v3u32 __attribute__((ext_vector_type(3)));
                         const v3u32 t3 = __builtin_amdgcn_raw_buffer_load_b96(
                             RF, (V.cur + pl * V.osize + rr * V.sp + c - 1) * 4, 0, 0);
                         a0 = __uint_as_float(t3.x); a1 = __uint_as_float(t3.y); a2 = __uint_as_float(t3.z);
+#endif
                     }
 #endif
                     test(at, a0); test(at + 1, a1); test(at + 2, a2);
