@@ -75,9 +75,9 @@ def test_scanner_rule(tmp_path):
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="libsurfhip.so not built")
-def test_built_library_has_no_exposed_wide_store():
+def test_built_library_has_no_exposed_wide_store(tmp_path):
     sc = _scanner()
-    files = sc.disassemble_lib(LIB)
+    files = sc.disassemble_lib(LIB, str(tmp_path))
     assert files, "no gfx950 code object found in libsurfhip.so"
     total, nstores, where = 0, 0, []
     for f in files:

@@ -39,10 +39,11 @@ FUNC = re.compile(r"^(?:[0-9a-f]+ <(\S+)>|(_Z\S+|\w+)):\s*(;.*)?$")
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 
 
-def disassemble_lib(lib: str) -> list[str]:
+def disassemble_lib(lib: str, tmp: str | None = None) -> list[str]:
     """The gfx950 code objects bundled in a HIP shared library, disassembled
-    (llvm-objdump extracts the bundles next to its input: work on a copy)."""
-    tmp = tempfile.mkdtemp(prefix="hzscan")
+    into `tmp` (a new temporary directory when None; llvm-objdump extracts
+    the bundles next to its input: work on a copy)."""
+    tmp = tmp or tempfile.mkdtemp(prefix="hzscan")
     cp = os.path.join(tmp, "lib.so")
     shutil.copyfile(lib, cp)
     subprocess.run([OBJDUMP, "--offloading", cp], cwd=tmp, check=True, capture_output=True)
