@@ -86,7 +86,7 @@ struct surfhip_detector {
     int nitems = 0;                     // scan items per frame
     int* offsets = nullptr;
     int* order = nullptr;               // per frame: keypoint indices in row order (describe schedule)
-    float4* work = nullptr;             // the describe schedule flattened: 2 float4 per keypoint (k_worklist)
+    float4* work = nullptr;             // the describe schedule flattened: kWorkF4 float4 per keypoint (k_worklist)
     int* status = nullptr;
     // single-frame API slots
     surfhip_point* pts1 = nullptr;
@@ -517,7 +517,7 @@ int surfhip_detector_create(surfhip_detector** out, const surfhip_param* param, 
     ALLOC(d->item_off, (2 * B * (size_t)d->nitems + 64) * sizeof(int));
     ALLOC(d->offsets, (B + 1) * sizeof(int));
     ALLOC(d->order, B * (size_t)max_pts * sizeof(int));
-    ALLOC(d->work, B * (size_t)max_pts * 2 * sizeof(float4));
+    ALLOC(d->work, B * (size_t)max_pts * kWorkF4 * sizeof(float4));
     ALLOC(d->status, 256 + kDescQueueBytes);    // [0]: flags; from [64]: describe work queues
     ALLOC(d->pts1, (size_t)max_pts * sizeof(surfhip_point));
     ALLOC(d->desc1, (size_t)max_pts * d->param.nfeatures * sizeof(float));
@@ -803,9 +803,11 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
     }();
     const bool pref_nms = pref_env < 0 ? !iiw : pref_env == 1;
     if (pipe && pref_nms) HIPCHK(prefetch_next());
+    // getTrace in k_describe_u2 (its integral rows are in L2 there) rather
+    // than in the fit (16 scattered integral loads per survivor from HBM)
+    const bool trace_desc = desc && trace_in_describe(d->P, nframes);
     HIPCHK(launch_nms(d->ii, d->resp, nframes, d->P, d->d_oct, d->plan, d->scan_key, d->scan_src, d->scan_cube,
-                      d->item_count,
-                      d->item_off, d->cand, d->keys, d->cand_count, d->cap, d->status, s));
+                      d->item_count, d->item_off, d->cand, d->keys, d->cand_count, d->cap, d->status, s, trace_desc));
     if (prof) HIPCHK(hipEventRecord(d->ev[3], s));
     HIPCHK(launch_sort(d->cand, d->keys, d->gscratch, d->cand_count, d->item_off, d->plan.nms_start[kMaxOct] * 4,
                        d->cap, nframes, points, d->max_pts, counts, d->offsets, d->order, d->status, s));
@@ -814,7 +816,7 @@ int surfhip_detect_batch_next(surfhip_detector* d, const uint8_t* frames, int nf
     if (d->desc_ev) HIPCHK(hipEventRecord(d->desc_ev, s));
     if (desc)
         HIPCHK(launch_describe(d->ii, d->P, points, d->max_pts, counts, d->offsets, d->order, d->work, nframes, desc,
-                               d->status + 64, s, pipe && !pref_nms && !iiw, d->cus));
+                               d->status + 64, s, pipe && !pref_nms && !iiw, d->cus, trace_desc));
     if (prof) HIPCHK(hipEventRecord(d->ev[5], s));
     d->last_nframes = nframes;
     d->last_frames = frames;

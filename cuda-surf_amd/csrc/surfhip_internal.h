@@ -136,6 +136,8 @@ inline bool plan_reads_frames(const LaunchPlan& p) { return p.q0 || p.q1 || p.hw
 // frames (measured crossover, 1080p: gather 9,956 vs streaming 7,981 frames/s
 // at 8 frames, 12,474 vs 14,085 at 16).
 constexpr int kGatherBatch = 8;
+// float4s per k_worklist entry (k_describe_u2's flattened schedule)
+constexpr int kWorkF4 = 3;
 void make_plan(const FrameParams& P, const OctaveParams* oct, LaunchPlan& plan, int max_batch);
 // the Hessian stage's kernels of a plan, as text (surfhip_hessian_plan)
 std::string hessian_plan_text(const LaunchPlan& plan, const FrameParams& P);
@@ -160,7 +162,7 @@ hipError_t launch_rowseg(const uint8_t* frames, int pitch, long long fstride, in
 hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,
                       const OctaveParams* d_oct, const LaunchPlan& plan, uint32_t* scan_key, uint32_t* scan_src,
                       float* scan_cube, int* item_count, int* item_off, surfhip_point* cand, uint32_t* keys,
-                      int* cand_count, int cap, int* status, hipStream_t s);
+                      int* cand_count, int cap, int* status, hipStream_t s, bool stash_trace);
 hipError_t launch_sort(const surfhip_point* cand, const uint32_t* keys, uint64_t* gscratch,
                        const int* cand_count, const int* soff, int items_per_frame, int cap, int nframes,
                        surfhip_point* out, int max_pts, int* out_count, int* offsets, int* order, int* status,
@@ -170,11 +172,21 @@ hipError_t set_max_lds(const void* fn, int bytes);
 // k_describe_ur, 8 x kDescQ of them 256 B apart, zeroed by the launch)
 // beside: another stream's kernels (the next batch's integral) run beside
 // it, so the persistent grid leaves each CU a workgroup slot
-// work: max_batch * max_pts float4 of scratch (k_describe_u2's flattened schedule)
+// work: max_batch * max_pts * kWorkF4 float4 of scratch (k_describe_u2's flattened schedule)
 // cus: compute units of the detector's device (sizes the persistent grid)
+// trace: the fit left getTrace to the describe (trace_in_describe, the same
+// call's stash_trace of launch_nms)
 hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
                            const int* counts, const int* offsets, const int* order, float4* work, int nframes,
-                           float* desc, int* queue, hipStream_t s, bool beside, int cus);
+                           float* desc, int* queue, hipStream_t s, bool beside, int cus, bool trace);
+// Whether a batch of nframes describes on k_describe_u2 (upright 4 x 4
+// windows, batches > kGatherBatch or SURFHIP_DESC_UR=0, packed worklist
+// fields large enough), and whether its laplace sign (getTrace,
+// surfd.cu:369-377) is then taken there, from the integral rows the
+// keypoint's window brings into L2, instead of in k_nms_fit
+// (SURFHIP_TRACE_DESC=0: in the fit, A/B)
+bool describe_on_u2(const FrameParams& P, int nframes);
+bool trace_in_describe(const FrameParams& P, int nframes);
 // Doubled-image input (surfhip_double.hip): frames (W x H) -> D ((2W-2) x
 // (2H-2) u8, row pitch dpitch, a multiple of 4).
 // HBM stream-rate kernels (surfhip_stream.hip): mode 0 copy, 1 read, 2 write

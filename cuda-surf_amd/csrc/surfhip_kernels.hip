@@ -1092,9 +1092,12 @@ __device__ __forceinline__ int32_t trace_sign(const uint32_t* __restrict__ I, in
 // 942-1022) for one NMS survivor.
 // cube: the scan's record of the 19 responses around (s, r, c) (nullptr:
 // read them from the planes)
+// stash: leave getTrace to k_describe_u2 (trace_in_describe): laplace holds
+// its box centre x0 | y0 << 16 (int16 each) and ori the lobe `temp`, which
+// the describe kernel replaces by the sign and 0
 __device__ bool nms_fit_point(const uint32_t* __restrict__ I, const OctView& V, const FrameParams& P,
                               const OctaveParams& q, int o, int s, int r, int c, const float4* cube,
-                              surfhip_point& pt)
+                              surfhip_point& pt, bool stash)
 {
     const int sw = q.sw, sh = q.sh;
     float off[3] = {0.f, 0.f, 0.f};
@@ -1152,7 +1155,12 @@ __device__ bool nms_fit_point(const uint32_t* __restrict__ I, const OctView& V, 
     v[6] = v[0] - temp;
     v[7] = v[1] + temp;
     v[8] = v[1] - temp;
-    pt.laplace = trace_sign(I, P.ip, P.iH * P.ip, v);
+    if (stash) {
+        pt.laplace = (int)(((uint32_t)v[0] & 0xffffu) | ((uint32_t)v[1] << 16));
+        pt.ori = __int_as_float(temp);
+    } else {
+        pt.laplace = trace_sign(I, P.ip, P.iH * P.ip, v);
+    }
     return true;
 }
 
@@ -1567,7 +1575,7 @@ __global__ __launch_bounds__(256) void k_nms_fit(const int32_t* __restrict__ ii,
                                                  const float* __restrict__ scan_cube,
                                                  const int* __restrict__ soff, int nitems, int items_per_frame,
                                                  surfhip_point* __restrict__ cand, uint32_t* __restrict__ keys,
-                                                 int* __restrict__ cand_count, int cap)
+                                                 int* __restrict__ cand_count, int cap, int stash)
 {
     const int total = soff[nitems];
     const int stride = (int)gridDim.x * 256;
@@ -1597,7 +1605,7 @@ __global__ __launch_bounds__(256) void k_nms_fit(const int32_t* __restrict__ ii,
                 ? reinterpret_cast<const float4*>(scan_cube + ((size_t)lo * kCubeCap + idx) * kCubeF) : nullptr;
 #ifndef SURF_DIAG_NOFIT
             ok = nms_fit_point(I, V, P, q, o, (int)(src >> 28), (int)((src >> 14) & 0x3fffu), (int)(src & 0x3fffu),
-                               cube, pt);
+                               cube, pt, stash != 0);
 #else
             ok = (src & 1u) && I != nullptr && V.F != nullptr && cube != nullptr;
 #endif
@@ -1631,7 +1639,7 @@ __global__ __launch_bounds__(256) void k_nms_fit(const int32_t* __restrict__ ii,
 hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const FrameParams& P,
                       const OctaveParams* d_oct, const LaunchPlan& plan, uint32_t* scan_key, uint32_t* scan_src,
                       float* scan_cube, int* item_count, int* item_off, surfhip_point* cand, uint32_t* keys,
-                      int* cand_count, int cap, int* status, hipStream_t s)
+                      int* cand_count, int cap, int* status, hipStream_t s, bool stash_trace)
 {
     const int per = plan.nms_start[kMaxOct];
     if (per == 0) {
@@ -1652,8 +1660,7 @@ hipError_t launch_nms(const int32_t* ii, const float* resp, int nframes, const F
     const int nitems = nframes * per * 4;
     launch_excl_scan(item_count, nitems, item_off, item_off + nitems + 1, s);
     k_nms_fit<<<fit_grid(), 256, 0, s>>>(ii, resp, P, d_oct, scan_key, scan_src, scan_cube, item_off, nitems, per * 4,
-                                         cand, keys,
-                                       cand_count, cap);
+                                         cand, keys, cand_count, cap, stash_trace ? 1 : 0);
     return hipGetLastError();
 }
 
@@ -3306,10 +3313,13 @@ __global__ __launch_bounds__(256) void k_worklist(const surfhip_point* __restric
                                                   FrameParams P)
 {
     // a frame's entries over gridDim.x workgroups, strided (most of a
-    // max_pts-sized grid would find nothing to do).  Entry = two float4 of
+    // max_pts-sized grid would find nothing to do).  Entry = three float4:
     // the keypoint's window geometry, the describe kernel's per-keypoint
-    // set-up moved here (surfd.cu:1581-1596, the upright branch of describe):
+    // set-up moved here (surfd.cu:1581-1596, the upright branch of describe),
+    // then the point's laplace / ori words (getTrace's inputs when the fit
+    // left it to the describe, nms_fit_point):
     //   {dx, dy, spacing, f}  {ix, iy, step | hs << 10 | iradius << 22, f * max_pts + kp}
+    //   {laplace, ori, 0, 0}
     // (10 / 12 / 10 bits: launch_describe takes this path only when the
     // largest window of the detector's octaves fits, worklist_fits)
     const int f = blockIdx.y, n = counts[f], o = offsets[f];
@@ -3323,10 +3333,11 @@ __global__ __launch_bounds__(256) void k_worklist(const surfhip_point* __restric
         const float spacing = scale * (float)P.mag;
         const int hs = f2i_rz(scale);
         const int iradius = f2i_rn(((spacing * (float)(P.wsz + 1)) * 0.5f) / (float)step);
-        work[2 * (size_t)(o + i)] = make_float4(at.x - (float)ix, at.y - (float)iy, spacing, __int_as_float(f));
-        work[2 * (size_t)(o + i) + 1] =
-            make_float4(__int_as_float(ix), __int_as_float(iy), __int_as_float(step | (hs << 10) | (iradius << 22)),
-                        __int_as_float(idx));
+        float4* e = work + kWorkF4 * (size_t)(o + i);
+        e[0] = make_float4(at.x - (float)ix, at.y - (float)iy, spacing, __int_as_float(f));
+        e[1] = make_float4(__int_as_float(ix), __int_as_float(iy), __int_as_float(step | (hs << 10) | (iradius << 22)),
+                           __int_as_float(idx));
+        e[2] = make_float4(__int_as_float(p.laplace), p.ori, 0.f, 0.f);
     }
 }
 
@@ -3346,9 +3357,27 @@ static bool worklist_fits(const FrameParams& P)
     return S * 0.5f + 1.f < 1024.f && S + 1.f < 4096.f && iradius < 1024.f;
 }
 
+bool describe_on_u2(const FrameParams& P, int nframes)
+{
+    // SURFHIP_DESC_UR=1 / 0 forces k_describe_ur / k_describe_u2 (read per
+    // call, so a process can A/B both kernels); default: k_describe_ur for
+    // batches of <= kGatherBatch frames, where a wave gets about one keypoint
+    // and the ring's fill latency is not amortised -- one 1080p frame's
+    // describe 0.032 -> 0.030 ms
+    const char* ur = getenv("SURFHIP_DESC_UR");
+    const bool use_u2 = ur ? atoi(ur) == 0 : nframes > kGatherBatch;
+    return P.upright && P.wsz == 4 && use_u2 && worklist_fits(P);
+}
+
+bool trace_in_describe(const FrameParams& P, int nframes)
+{
+    const char* e = getenv("SURFHIP_TRACE_DESC");
+    return (e ? atoi(e) != 0 : true) && describe_on_u2(P, nframes);
+}
+
 hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_point* pts, int max_pts,
                            const int* counts, const int* offsets, const int* order, float4* work, int nframes,
-                           float* desc, int* queue, hipStream_t s, bool beside, int cus)
+                           float* desc, int* queue, hipStream_t s, bool beside, int cus, bool trace)
 {
     if (P.nfeat > 512) return hipErrorInvalidValue;
     // the describe kernels are persistent (per-XCD keypoint queues): 2,048
@@ -3359,21 +3388,19 @@ hipError_t launch_describe(const int32_t* ii, const FrameParams& P, surfhip_poin
     const int grid = (beside && per_cu > 0) ? ((per_cu * cus + 7) & ~7) : 2048;
     hipError_t e = hipMemsetAsync(queue, 0, kDescQueueBytes, s);
     if (e != hipSuccess) return e;
-    // k_describe_u2 (LDS-DMA ring); SURFHIP_DESC_UR=1: round 3's
-    // k_describe_ur (read per launch, so a process can A/B both kernels)
-    // (SURFHIP_DESC_UR=1 / 0 forces k_describe_ur / k_describe_u2; default:
-    // k_describe_ur for batches of <= kGatherBatch frames, where a wave gets
-    // about one keypoint and the ring's fill latency is not amortised --
-    // one 1080p frame's describe 0.032 -> 0.030 ms)
-    const char* ur = getenv("SURFHIP_DESC_UR");
-    const bool use_u2 = ur ? atoi(ur) == 0 : nframes > kGatherBatch;
-    if (P.upright && P.wsz == 4 && use_u2 && worklist_fits(P)) {
+    // k_describe_u2 (LDS-DMA ring), else round 3's k_describe_ur
+    // (describe_on_u2); `trace` implies the u2 path (trace_in_describe)
+    const bool u2 = describe_on_u2(P, nframes);
+    if (trace && !u2) return hipErrorInvalidValue;
+    if (u2) {
         k_worklist<<<dim3(std::min(8, (max_pts + 255) / 256), nframes), 256, 0, s>>>(pts, max_pts, counts, offsets,
                                                                                       order, work, P);
         // (diagnostic: SURFHIP_U2_LDSPAD bytes of unused dynamic LDS per workgroup)
         static const int pad = getenv("SURFHIP_U2_LDSPAD") ? atoi(getenv("SURFHIP_U2_LDSPAD")) : 0;
-        if (P.extend) k_describe_u2<true><<<grid, 256, pad, s>>>(ii, P, work, max_pts, offsets, nframes, desc, queue);
-        else k_describe_u2<false><<<grid, 256, pad, s>>>(ii, P, work, max_pts, offsets, nframes, desc, queue);
+        const int tr = trace ? 1 : 0;
+        if (P.extend)
+            k_describe_u2<true><<<grid, 256, pad, s>>>(ii, P, work, max_pts, offsets, nframes, desc, queue, pts, tr);
+        else k_describe_u2<false><<<grid, 256, pad, s>>>(ii, P, work, max_pts, offsets, nframes, desc, queue, pts, tr);
     } else if (P.upright && P.wsz == 4) {
         if (P.extend)
             k_describe_ur<true><<<grid, 256, 0, s>>>(ii, P, pts, max_pts, offsets, order, nframes, desc, queue);

@@ -221,6 +221,29 @@ def test_fit_records_from_scan(surf, orc, monkeypatch, cube):
         compare_frame(res["pts"][f], res["desc"][f], o_pts, o_desc, True)
 
 
+@pytest.mark.parametrize("trace_desc,desc", [("1", True), ("0", True), ("1", False)])
+def test_laplace_in_fit_or_describe(surf, orc, monkeypatch, trace_desc, desc):
+    """makePoint's laplace (getTrace, surfd.cu:369-377, 1010-1020) taken in
+    k_describe_u2 from the fit's stashed inputs (SURFHIP_TRACE_DESC=1, the
+    default when k_describe_u2 runs), in k_nms_fit (=0), and in the fit when
+    no descriptors are asked for: every point field equals the oracle's,
+    laplace and ori (0) included, bit for bit."""
+    monkeypatch.setenv("SURFHIP_TRACE_DESC", trace_desc)
+    w, h = 640, 480
+    frames = surf.synth_frames(12, w, h, first=700)
+    param = surf.make_param(4, 4.0, upright=True)
+    res = gpu_run(surf, param, frames, w, h, desc=desc)
+    op = orc.make_param(4, 4.0, upright=True)
+    for f in (0, 5, 11):
+        o_pts, o_desc, nc = orc.detect(op, frames[f], w, h)
+        assert res["cand"][f] == nc
+        assert_points_equal(res["pts"][f], o_pts)
+        assert (res["pts"][f]["ori"] == 0).all()
+        assert set(np.unique(res["pts"][f]["laplace"])) <= {-1, 1}
+        if desc:
+            compare_frame(res["pts"][f], res["desc"][f], o_pts, o_desc, True)
+
+
 @pytest.mark.parametrize("extend", [False, True])
 @pytest.mark.parametrize("atomic", [False, True])
 def test_rotated_descriptor_kernels(surf, orc, monkeypatch, extend, atomic):
