@@ -3319,7 +3319,7 @@ __global__ __launch_bounds__(256) void k_worklist(const surfhip_point* __restric
     // then the point's laplace / ori words (getTrace's inputs when the fit
     // left it to the describe, nms_fit_point):
     //   {dx, dy, spacing, f}  {ix, iy, step | hs << 10 | iradius << 22, f * max_pts + kp}
-    //   {laplace, ori, 0, 0}
+    //   {laplace, ori, 1 / spacing, 0}
     // (10 / 12 / 10 bits: launch_describe takes this path only when the
     // largest window of the detector's octaves fits, worklist_fits)
     const int f = blockIdx.y, n = counts[f], o = offsets[f];
@@ -3337,7 +3337,7 @@ __global__ __launch_bounds__(256) void k_worklist(const surfhip_point* __restric
         e[0] = make_float4(at.x - (float)ix, at.y - (float)iy, spacing, __int_as_float(f));
         e[1] = make_float4(__int_as_float(ix), __int_as_float(iy), __int_as_float(step | (hs << 10) | (iradius << 22)),
                            __int_as_float(idx));
-        e[2] = make_float4(__int_as_float(p.laplace), p.ori, 0.f, 0.f);
+        e[2] = make_float4(__int_as_float(p.laplace), p.ori, 1.f / spacing, 0.f);
     }
 }
 
