@@ -3329,7 +3329,13 @@ __global__ __launch_bounds__(256) void k_worklist(const surfhip_point* __restric
         const DescAt at = desc_at(P.doubled, p);
         const float scale = at.scale;
         const int step = max(f2i_rn(scale * 0.5f), 1);
+#ifdef SURF_DIAG_WL_SAMEPOS
+        // (diagnostic: every window of a frame at the frame's centre -- its
+        // rows stay in L2; wrong descriptors, the same work)
+        const int ix = P.W / 2, iy = P.H / 2;
+#else
         const int ix = f2i_rn(at.x), iy = f2i_rn(at.y);
+#endif
         const float spacing = scale * (float)P.mag;
         const int hs = f2i_rz(scale);
         const int iradius = f2i_rn(((spacing * (float)(P.wsz + 1)) * 0.5f) / (float)step);
