@@ -317,12 +317,6 @@ static int derive(surfhip_detector* d)
     P.H = d->H;
     const int iw = d->W + 1, ih = d->H + 1;
     P.ip = align_up(iw, 128);
-    {
-        // (experiment: SURFHIP_II_PAD extra ints per integral row, a multiple of 4)
-        const char* e = getenv("SURFHIP_II_PAD");
-        const int pad = e ? atoi(e) : 0;
-        if (pad > 0 && pad % 4 == 0) P.ip += pad;
-    }
     P.iH = ih;
     P.ii_stride = (long long)ih * P.ip;
     P.max_scale = p.max_scale;
