@@ -22,7 +22,10 @@ constexpr int kMaxOct = 8;
 constexpr int kMaxScale = 8;
 constexpr int kSortCap = 16384;     // candidates per frame sorted in LDS
 constexpr uint32_t kNoKey = 0xffffffffu;   // candidate slot of a rejected NMS survivor
-constexpr int kDescQ = 16;                  // describe work queues per XCD
+#ifndef SURF_DESC_Q
+#define SURF_DESC_Q 16                      // (A/B: <= 16; the queue memset covers 16)
+#endif
+constexpr int kDescQ = SURF_DESC_Q;         // describe work queues per XCD
 constexpr int kDescQueueBytes = 8 * kDescQ * 64 * 4;
 constexpr int kBandRows = 32;       // integral-image band height
 constexpr int kBandRowsSmall = 16;  // ... for batches of <= kSmallBatch frames (one 1080p frame: 16 -> 0.1281-0.1287 ms vs 8 -> 0.1298-0.1305, 4 -> 0.131)
