@@ -1586,11 +1586,42 @@ __global__ __launch_bounds__(256) void k_nms_fit(const int32_t* __restrict__ ii,
         surfhip_point pt;
         bool ok = false;
         uint32_t key = 0;
+        // the scan item holding each lane's survivor t = base + lane: the
+        // wave finds base's item by a 64-way search (one coalesced load of
+        // 64 probes per level: ~3-4 levels instead of a lane's ~19 dependent
+        // loads), then lane t counts the item starts after it that are <= t
+        // among the next 64 (ascending: a 6-step search over the lanes'
+        // values); a lane past those 64 items searches on its own
+        int wlo = 0;
+        {
+            int hi = nitems;                                 // soff[wlo] <= base < soff[hi]
+            while (hi - wlo > 1) {
+                const int sw = (hi - wlo + 63) >> 6;
+                const int pr = wlo + ((int)lane_id() + 1) * sw;
+                const bool le = pr < hi && soff[pr] <= base;
+                const unsigned long long m = __ballot(le);
+                const int k = m ? 64 - __builtin_clzll(m) : 0;
+                wlo += k * sw;
+                hi = min(wlo + sw, hi);
+            }
+        }
+        const int wi = wlo + 1 + (int)lane_id();
+        const int wst = wi <= nitems ? soff[wi] : 0x7fffffff; // item starts after wlo, ascending
+        int cnt = 0;
+#pragma unroll
+        for (int sft = 32; sft >= 1; sft >>= 1) {
+            const int v = __shfl(wst, cnt + sft - 1, 64);
+            if (v <= t) cnt += sft;
+        }
+        if (cnt == 63 && __shfl(wst, 63, 64) <= t) cnt = 64;      // (all 64 starts <= t)
         if (act) {
-            int lo = 0, hi = nitems;                     // scan item holding survivor t
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (soff[mid] <= t) lo = mid; else hi = mid;
+            int lo = wlo + cnt;                          // scan item holding survivor t
+            if (cnt == 64) {
+                int hi = nitems;
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (soff[mid] <= t) lo = mid; else hi = mid;
+                }
             }
             f = lo / items_per_frame;
             const int idx = t - soff[lo];                // survivor index within its scan item
